@@ -1,0 +1,258 @@
+"""RS(10,4) encode+decode throughput on MI355X (device-resident), the metric of
+BASELINE.json: "RS(10,4) encode+decode GiB/s (device-resident), 1 MiB stripes,
+1/2/4/8 GPUs".
+
+One step = one pass of the hot path over one batch: encode every stripe of a
+[4096, 14, 1 MiB] HBM-resident batch (10 data shards -> 4 parity, one
+hec_gpu_encode_batch launch), then reconstruct every stripe with 4 random
+erasures (one hec_gpu_reconstruct_batch launch; each stripe reads its first 10
+survivors and rewrites its 4 erased shards). Inputs are synthetic splitmix64
+stripes generated in HBM before the timed region.
+
+value = data-payload GiB/s over all ranks: (encode 10*L + decode 10*L bytes
+per stripe) * stripes * ranks / max-over-ranks step time. Multi-GPU: one
+process per GPU (torchrun), independent stripe batches per rank (seed base
+0x5EED0000 + rank*2^20), no data-path collective ("scaling": "weak"); the
+only cross-rank traffic is the barrier and the max-reduce of the timings.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+K_DATA, M_PARITY, N_TOTAL = 10, 4, 14
+HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E, GB/s (MI355X_MICROARCH.md)
+SEED_BASE = 0x5EED0000
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def rank_seed_base(rank: int) -> int:
+    return SEED_BASE + rank * (1 << 20)
+
+
+def erasure_masks(n_stripes: int, rank: int, erasures: int = 4) -> np.ndarray:
+    """Per-stripe present masks with `erasures` shards dropped, uniform over the
+    C(14, erasures) patterns, seeded per rank."""
+    rng = np.random.default_rng(0xEC0000 + rank)
+    full = (1 << N_TOTAL) - 1
+    masks = np.empty(n_stripes, dtype=np.int32)
+    for s in range(n_stripes):
+        drop = rng.choice(N_TOTAL, erasures, replace=False)
+        m = full
+        for i in drop:
+            m &= ~(1 << int(i))
+        masks[s] = m
+    return masks
+
+
+def reduce_max(x: float, world: int) -> float:
+    """Max over ranks of a host scalar (control plane only: gloo all_reduce)."""
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return float(v.item())
+
+
+def job_throughput(payload_bytes_per_rank_step: float, steps: int, world: int, t_job: float) -> float:
+    """Whole-job GiB/s: every rank processes the same payload per step; the
+    job's time is the max over ranks."""
+    return payload_bytes_per_rank_step * steps * world / t_job / 2**30
+
+
+def cpu_baseline(seconds: float = 10.0) -> dict:
+    """helyim-ec's CPU path restated (oracle/rs_oracle.c, AVX2 nibble-pshufb,
+    upstream code_some_slices loop order), 1 thread: encode + 4-erasure
+    reconstruct of 1 MiB stripes, cycled over 8 distinct stripes for ~seconds."""
+    from oracle import corc
+    L = 1 << 20
+    rs = corc.CReedSolomon(K_DATA, M_PARITY)
+    stripes = []
+    rng = np.random.default_rng(11)
+    for s in range(8):
+        d = corc.splitmix64_bytes(SEED_BASE + s, K_DATA * L).reshape(K_DATA, L)
+        sh = [d[i].copy() for i in range(K_DATA)] + [np.zeros(L, np.uint8) for _ in range(M_PARITY)]
+        drop = sorted(rng.choice(N_TOTAL, 4, replace=False).tolist())
+        stripes.append((sh, [i not in drop for i in range(N_TOTAL)]))
+    simd = bool(corc.lib().orc_have_avx2())
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        sh, present = stripes[n % len(stripes)]
+        rs.encode(sh, simd=simd)
+        rs.reconstruct(sh, present, simd=simd)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gib = n * 2 * K_DATA * L / 2**30
+    return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{n} stripe encode+decode passes (10 x 1 MiB data, 4 erasures), 8 distinct "
+                      f"splitmix64 stripes cycled, {el:.1f} s, 1 thread, "
+                      f"{'AVX2 nibble-pshufb' if simd else 'scalar table'} C restatement of "
+                      f"helyim-ec/reed-solomon-erasure (oracle/rs_oracle.c)",
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_traffic() -> dict:
+    """HBM traffic per launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--shard-len", type=int, default=1 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(local_rank)
+
+    import helyim_amd as H
+    import helyim_amd.batch as B
+
+    S, L = args.stripes, args.shard_len
+    rs = H.ReedSolomon(K_DATA, M_PARITY)
+    t = torch.empty((S, N_TOTAL, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t, K_DATA * L, rank_seed_base(rank))
+    masks = torch.from_numpy(erasure_masks(S, rank)).cuda()
+    stream = torch.cuda.current_stream()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        B.encode_batch(rs, t)
+        B.reconstruct_batch(rs, t, masks)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        B.encode_batch(rs, t)
+        ev[i][1].record(stream)
+        B.reconstruct_batch(rs, t, masks)
+        ev[i][2].record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    t_job = reduce_max(wall, world)
+
+    # correctness of what was timed: zero the erased shards, rebuild, compare
+    full = (1 << N_TOTAL) - 1
+    chk_ok = True
+    sample = slice(0, min(S, 256))
+    ref_par = t[sample, K_DATA:].clone()
+    er = torch.zeros((S, N_TOTAL), dtype=torch.bool, device="cuda")
+    for i in range(N_TOTAL):
+        er[:, i] = (masks & (1 << i)) == 0
+    snap = t[sample][er[sample]].clone()
+    sub = t[sample]
+    sub[er[sample]] = 0
+    t[sample] = sub
+    B.reconstruct_batch(rs, t[sample], masks[sample])
+    torch.cuda.synchronize()
+    chk_ok &= bool(torch.equal(t[sample][er[sample]], snap))
+    chk_ok &= bool(torch.equal(t[sample, K_DATA:], ref_par))
+    if rank == 0:
+        from oracle import corc
+        ref = corc.encode_stripes(t[0:2, :K_DATA].cpu().numpy().copy())
+        chk_ok &= bool(np.array_equal(t[0:2, K_DATA:].cpu().numpy(), ref))
+    del t
+
+    enc_bytes = S * N_TOTAL * L                      # read 10 L + write 4 L per stripe
+    dec_bytes = S * (K_DATA + 4) * L                 # read 10 survivors + write 4 erased
+    payload = 2 * S * K_DATA * L                     # data-payload bytes per step (encode + decode)
+    value = job_throughput(payload, args.steps, world, t_job)
+    enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
+    dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
+    traffic = load_traffic().get("encode_hbm_bytes_per_launch")
+
+    if rank == 0:
+        out = {
+            "metric": "RS(10,4) encode+decode GiB/s (device-resident), 1 MiB stripes, 1/2/4/8 GPUs",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_job / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 stripes generated in HBM)",
+            "config": {"workload": f"RS(10,4) encode + 4-erasure decode, {S} stripes x {L} B shards per GPU "
+                                   f"(BASELINE configs 2+3), device-resident",
+                       "stripes_per_gpu": S, "shard_len": L, "erasures_per_stripe": 4,
+                       "parallelism": f"independent stripe batches x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(enc_gbps, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel": "rs_apply_kernel<10,U,true> (encode)",
+                         "algorithmic_bytes_per_launch": enc_bytes},
+            "encode": {"ms_per_launch": round(enc_ms, 4), "GB_s_hbm": round(enc_gbps, 1),
+                       "data_GiB_s": round(S * K_DATA * L / (enc_ms * 1e-3) / 2**30, 1)},
+            "decode": {"ms_per_launch": round(dec_ms, 4), "GB_s_hbm": round(dec_gbps, 1),
+                       "data_GiB_s": round(S * K_DATA * L / (dec_ms * 1e-3) / 2**30, 1),
+                       "frac": round(dec_gbps / HBM_PEAK_GBPS, 4)},
+            "verified": chk_ok,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not chk_ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

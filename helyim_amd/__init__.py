@@ -1,0 +1,30 @@
+"""helyim_amd -- MI355X-native RS(10,4) erasure coding for helyim's EC tier.
+
+Host mirror of the reference's operator surface for the hot path:
+
+* ``ReedSolomon`` -- reed_solomon_erasure::ReedSolomon<galois_8::Field>
+  (new / encode / verify / reconstruct / reconstruct_data);
+* ``write_ec_files`` / ``rebuild_ec_files`` / ``to_ext`` and the geometry
+  constants -- helyim_ec (helyim-ec/src/lib.rs, encoder.rs);
+* ``batch`` -- device-resident stripe batches (torch tensors on ROCm).
+
+All compute runs in helyim_amd/libhec.so (HIP, gfx950). Import fails if the
+library is missing; there is no CPU fallback.
+"""
+from ._lib import LIB_PATH, lib  # noqa: F401  (raises ImportError when not built)
+from .errors import (  # noqa: F401
+    DeviceError, EcShardError, EmptyShard, ErasureCoding, Error, IncorrectShardSize, InvalidIndex,
+    InvalidShardFlags, Io, TooFewBufferShards, TooFewDataShards, TooFewParityShards, TooFewShards,
+    TooFewShardsPresent, TooManyBufferShards, TooManyDataShards, TooManyParityShards, TooManyShards,
+    Underflow, UnexpectedBlockSize, UnexpectedEcShardSize,
+)
+from .rs import ReedSolomon  # noqa: F401
+from .ec import (  # noqa: F401
+    DATA_SHARDS_COUNT, ERASURE_CODING_LARGE_BLOCK_SIZE, ERASURE_CODING_SMALL_BLOCK_SIZE,
+    PARITY_SHARDS_COUNT, TOTAL_SHARDS_COUNT, generate_ec_files, rebuild_ec_files, to_ext,
+    write_ec_files,
+)
+
+
+def version() -> str:
+    return lib.hec_version().decode()

@@ -1,0 +1,64 @@
+"""Loader for the in-tree HIP library helyim_amd/libhec.so (C ABI: include/hec.h).
+
+There is no fallback: if the library is missing or fails to load, importing
+helyim_amd raises. Compute calls without a GPU return HEC_ERR_NO_DEVICE, which
+surfaces as ``helyim_amd.errors.DeviceError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhec.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build the HIP library first (`make -C {os.path.dirname(_HERE)}` "
+        "or __graft_entry__.build()). helyim_amd has no CPU fallback."
+    )
+
+lib = ctypes.CDLL(LIB_PATH)
+
+_P = ctypes.c_void_p
+_S = ctypes.c_size_t
+_U64 = ctypes.c_uint64
+_U32 = ctypes.c_uint32
+_I = ctypes.c_int
+
+# name -> (restype, argtypes); every function declared in include/hec.h
+SIGNATURES = {
+    "hec_strerror": (ctypes.c_char_p, [_I]),
+    "hec_last_error_detail": (ctypes.c_char_p, []),
+    "hec_rs_new": (_I, [_S, _S, ctypes.POINTER(_P)]),
+    "hec_rs_free": (None, [_P]),
+    "hec_rs_data_shard_count": (_S, [_P]),
+    "hec_rs_parity_shard_count": (_S, [_P]),
+    "hec_rs_total_shard_count": (_S, [_P]),
+    "hec_rs_matrix": (_I, [_P, _P, _S]),
+    "hec_rs_encode": (_I, [_P, _P, _P, _S]),
+    "hec_rs_verify": (_I, [_P, _P, _P, _S, ctypes.POINTER(_I)]),
+    "hec_rs_reconstruct": (_I, [_P, _P, _P, _P, _S]),
+    "hec_rs_reconstruct_data": (_I, [_P, _P, _P, _P, _S]),
+    "hec_gpu_encode_batch": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32, _P]),
+    "hec_gpu_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P]),
+    "hec_gpu_fill_splitmix": (_I, [_P, _U64, _U64, _U32, _U64, _P]),
+    "hec_write_ec_files": (_I, [ctypes.c_char_p]),
+    "hec_write_ec_files_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64]),
+    "hec_rebuild_ec_files": (_I, [ctypes.c_char_p, ctypes.POINTER(_U32), ctypes.POINTER(_S)]),
+    "hec_set_launch_config": (_I, [_I, ctypes.c_long]),
+    "hec_version": (ctypes.c_char_p, []),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+def strerror(code: int) -> str:
+    return lib.hec_strerror(code).decode()
+
+
+def last_detail() -> str:
+    return lib.hec_last_error_detail().decode()

@@ -1,0 +1,72 @@
+"""Device-resident stripe batches over torch tensors (ROCm).
+
+PyTorch is plumbing here: it owns the HBM allocation and the HIP stream; the
+arithmetic is libhec's gfx950 kernels (hec_gpu_encode_batch /
+hec_gpu_reconstruct_batch). Layout: a uint8 tensor ``[S, total, L]`` (stripe
+major, shard, byte) -- a small row of the reference's .dat layout is exactly
+10 contiguous L-byte blocks, so a run of rows lands here with one copy.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .errors import check
+from .rs import ReedSolomon
+
+lib = _lib.lib
+
+
+def _stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _check_stripes(t: torch.Tensor, rs: ReedSolomon):
+    if t.dtype != torch.uint8 or not t.is_cuda or t.dim() != 3:
+        raise TypeError("expected a uint8 CUDA tensor [stripes, shards, L]")
+    if t.stride(2) != 1:
+        raise ValueError("shard bytes must be contiguous")
+
+
+def encode_batch(rs: ReedSolomon, stripes: torch.Tensor, stream=None) -> None:
+    """Parity of every stripe of ``stripes[S, total, L]`` into shards data..total."""
+    _check_stripes(stripes, rs)
+    k = rs.data_shard_count()
+    S, n, L = stripes.shape
+    assert n == rs.total_shard_count()
+    st, sh = stripes.stride(0), stripes.stride(1)
+    base = stripes.data_ptr()
+    check(lib.hec_gpu_encode_batch(rs.handle, base, st, sh, base + k * sh, st, sh, L, S,
+                                   _stream_ptr(stream)))
+
+
+def encode_batch_sep(rs: ReedSolomon, data: torch.Tensor, parity: torch.Tensor, stream=None) -> None:
+    """data[S, k, L] -> parity[S, m, L] (separate buffers)."""
+    S, k, L = data.shape
+    check(lib.hec_gpu_encode_batch(rs.handle, data.data_ptr(), data.stride(0), data.stride(1),
+                                   parity.data_ptr(), parity.stride(0), parity.stride(1), L, S,
+                                   _stream_ptr(stream)))
+
+
+def reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks: torch.Tensor,
+                      bad_stripes: torch.Tensor = None, stream=None) -> None:
+    """Rebuild erased shards in place; present_masks int32 [S] (bit i = shard i present)."""
+    _check_stripes(stripes, rs)
+    S, n, L = stripes.shape
+    assert present_masks.is_cuda and present_masks.dtype == torch.int32 and present_masks.numel() == S
+    bad = bad_stripes.data_ptr() if bad_stripes is not None else None
+    check(lib.hec_gpu_reconstruct_batch(rs.handle, stripes.data_ptr(), stripes.stride(0),
+                                        stripes.stride(1), L, S, present_masks.data_ptr(), bad,
+                                        _stream_ptr(stream)))
+
+
+def fill_splitmix(t: torch.Tensor, bytes_per_stripe: int, seed_base: int, stream=None) -> None:
+    """Fill the first bytes_per_stripe bytes of each t[s] with splitmix64(seed_base + s)."""
+    S = t.shape[0]
+    check(lib.hec_gpu_fill_splitmix(t.data_ptr(), t.stride(0), bytes_per_stripe, S, seed_base,
+                                    _stream_ptr(stream)))
+
+
+def set_launch_config(vec_per_thread: int = 2, max_blocks: int = 0) -> None:
+    check(lib.hec_set_launch_config(vec_per_thread, max_blocks))

@@ -1,0 +1,510 @@
+// C ABI of libhec (include/hec.h): the ReedSolomon<galois_8::Field> surface
+// helyim-ec calls (encoder.rs:191,208-209,249-250,288;
+// helyim-store/src/erasure_coding/mod.rs:411-412,426), the device batch entry
+// points, and shared device state. All compute goes through the gfx950
+// kernels in rs_kernels.hip; there is no CPU fallback.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <tuple>
+
+#include "hec_internal.hpp"
+
+namespace hec {
+
+static thread_local std::string g_detail;
+
+void set_detail(const std::string& s) { g_detail = s; }
+
+int fail(int code, const std::string& detail) {
+    g_detail = detail;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_detail = std::string(what) + ": " + hipGetErrorString(e);
+    if (e == hipErrorOutOfMemory) return HEC_ERR_OUT_OF_MEMORY;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return HEC_ERR_NO_DEVICE;
+    return HEC_ERR_HIP;
+}
+
+LaunchConfig& launch_config() {
+    static LaunchConfig cfg;
+    return cfg;
+}
+
+int current_device(int* dev) {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        return fail(HEC_ERR_NO_DEVICE, "no HIP device visible (libhec has no CPU fallback)");
+    }
+    HEC_HIP(hipGetDevice(dev));
+    return HEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Plans
+// ---------------------------------------------------------------------------
+uint32_t HostPlans::add(const Mat& coefs, const std::vector<uint32_t>& in_ids,
+                        const std::vector<uint32_t>& out_ids) {
+    DevPlan p;
+    p.nin = uint32_t(in_ids.size());
+    p.nout = uint32_t(out_ids.size());
+    p.tab_off = uint32_t(tabs.size());
+    p.idx_off = uint32_t(idx.size());
+    for (uint32_t i = 0; i < p.nin; ++i)
+        for (uint32_t r = 0; r < p.nout; ++r) {
+            uint32_t t[kTabWords];
+            perm_tables(coefs.at(int(r), int(i)), t);
+            tabs.insert(tabs.end(), t, t + kTabWords);
+        }
+    idx.insert(idx.end(), in_ids.begin(), in_ids.end());
+    idx.insert(idx.end(), out_ids.begin(), out_ids.end());
+    plans.push_back(p);
+    return uint32_t(plans.size() - 1);
+}
+
+uint32_t HostPlans::add_noop(uint32_t nin) {
+    DevPlan p{nin, 0, uint32_t(tabs.size()), uint32_t(idx.size())};
+    plans.push_back(p);
+    return uint32_t(plans.size() - 1);
+}
+
+template <typename T>
+static int grow_upload(T*& dptr, size_t& cap, const T* src, size_t count, hipStream_t s) {
+    if (count == 0) return HEC_OK;
+    if (count > cap) {
+        if (dptr) HEC_HIP(hipFree(dptr));
+        dptr = nullptr;
+        cap = 0;
+        HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dptr), count * sizeof(T)));
+        cap = count;
+    }
+    HEC_HIP(hipMemcpyAsync(dptr, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+    return HEC_OK;
+}
+
+int DevicePlanSet::upload(const HostPlans& hp, const std::vector<uint32_t>* lut_host, hipStream_t s) {
+    int rc;
+    if ((rc = grow_upload(plans, cap_plans, hp.plans.data(), hp.plans.size(), s))) return rc;
+    if ((rc = grow_upload(tabs, cap_tabs, hp.tabs.data(), hp.tabs.size(), s))) return rc;
+    if ((rc = grow_upload(idx, cap_idx, hp.idx.data(), hp.idx.size(), s))) return rc;
+    if (lut_host && (rc = grow_upload(lut, cap_lut, lut_host->data(), lut_host->size(), s))) return rc;
+    // Host vectors may be freed by the caller right after: make the copies land.
+    HEC_HIP(hipStreamSynchronize(s));
+    return HEC_OK;
+}
+
+void DevicePlanSet::release() {
+    (void)hipFree(plans);
+    (void)hipFree(tabs);
+    (void)hipFree(idx);
+    (void)hipFree(lut);
+    plans = nullptr;
+    tabs = idx = lut = nullptr;
+    cap_plans = cap_tabs = cap_idx = cap_lut = 0;
+}
+
+// upstream reconstruct_internal: first k present shards -> sub-matrix ->
+// inverse; missing data rows = inverse rows; missing parity rows = parity
+// row x inverse (composed, bit-identical to upstream's second pass since the
+// reconstructed data bytes are unique).
+int decode_plan(const hec_rs* rs, const uint8_t* present, bool data_only, Mat& coefs,
+                std::vector<uint32_t>& in_ids, std::vector<uint32_t>& out_ids, bool* noop) {
+    const int k = rs->k, n = rs->n;
+    int npresent = 0;
+    for (int i = 0; i < n; ++i) npresent += present[i] ? 1 : 0;
+    *noop = false;
+    in_ids.clear();
+    out_ids.clear();
+    if (npresent == n) {
+        *noop = true;
+        return HEC_OK;
+    }
+    if (npresent < k) return HEC_ERR_TOO_FEW_SHARDS_PRESENT;
+    std::vector<uint32_t> miss;
+    for (int i = 0; i < n; ++i) {
+        if (present[i]) {
+            if (int(in_ids.size()) < k) in_ids.push_back(uint32_t(i));
+        } else {
+            miss.push_back(uint32_t(i));
+        }
+    }
+    Mat sub(k, k);
+    for (int r = 0; r < k; ++r)
+        for (int c = 0; c < k; ++c) sub.at(r, c) = rs->matrix.at(int(in_ids[r]), c);
+    Mat inv;
+    if (!mat_invert(sub, inv)) return fail(HEC_ERR_INVALID_ARGUMENT, "singular decode matrix");
+    for (uint32_t i : miss)
+        if (!(data_only && int(i) >= k)) out_ids.push_back(i);
+    coefs = Mat(int(out_ids.size()), k);
+    const Gf& g = gf();
+    for (size_t r = 0; r < out_ids.size(); ++r) {
+        const int id = int(out_ids[r]);
+        if (id < k) {
+            for (int c = 0; c < k; ++c) coefs.at(int(r), c) = inv.at(id, c);
+        } else {
+            for (int c = 0; c < k; ++c) {
+                uint8_t acc = 0;
+                for (int t = 0; t < k; ++t) acc ^= g.mul[rs->matrix.at(id, t)][inv.at(t, c)];
+                coefs.at(int(r), c) = acc;
+            }
+        }
+    }
+    if (out_ids.empty()) *noop = true;
+    return HEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Per-device geometry state
+// ---------------------------------------------------------------------------
+static std::mutex g_geom_mu;
+static std::map<std::tuple<int, int, int>, std::unique_ptr<GeomDevice>> g_geom;
+
+int geom_device(const hec_rs* rs, GeomDevice** out) {
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_geom_mu);
+    auto key = std::make_tuple(dev, rs->k, rs->m);
+    auto it = g_geom.find(key);
+    if (it != g_geom.end()) {
+        *out = it->second.get();
+        return HEC_OK;
+    }
+    std::unique_ptr<GeomDevice> gd(new GeomDevice());
+    HostPlans hp;
+    Mat par(rs->m, rs->k);
+    for (int r = 0; r < rs->m; ++r)
+        for (int c = 0; c < rs->k; ++c) par.at(r, c) = rs->matrix.at(rs->k + r, c);
+    std::vector<uint32_t> in_ids, out_ids;
+    for (int i = 0; i < rs->k; ++i) in_ids.push_back(uint32_t(i));
+    for (int j = 0; j < rs->m; ++j) out_ids.push_back(uint32_t(j));
+    hp.add(par, in_ids, out_ids);
+    if ((rc = gd->encode.upload(hp, nullptr, nullptr))) return rc;
+    *out = gd.get();
+    g_geom[key] = std::move(gd);
+    return HEC_OK;
+}
+
+int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_geom_mu);
+    if (gd->decode_ready) return HEC_OK;
+    const int n = rs->n, k = rs->k;
+    if (n > 16) return fail(HEC_ERR_INVALID_ARGUMENT, "device-mask reconstruct needs total shards <= 16");
+    HostPlans hp;
+    std::vector<uint32_t> lut(size_t(1) << n, kNoPlan);
+    const uint32_t noop = hp.add_noop(uint32_t(k));
+    uint8_t present[16];
+    Mat coefs;
+    std::vector<uint32_t> in_ids, out_ids;
+    for (uint32_t mask = 0; mask < (1u << n); ++mask) {
+        const int pc = __builtin_popcount(mask);
+        if (pc < k) continue;
+        if (pc == n) {
+            lut[mask] = noop;
+            continue;
+        }
+        for (int i = 0; i < n; ++i) present[i] = (mask >> i) & 1;
+        bool is_noop = false;
+        int rc = decode_plan(rs, present, false, coefs, in_ids, out_ids, &is_noop);
+        if (rc) return rc;
+        lut[mask] = hp.add(coefs, in_ids, out_ids);
+    }
+    int rc = gd->decode_dense.upload(hp, &lut, s);
+    if (rc) return rc;
+    gd->decode_ready = true;
+    return HEC_OK;
+}
+
+int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uint64_t in_stripe,
+              uint64_t in_shard, uint8_t* out_base, uint64_t out_stripe, uint64_t out_shard,
+              uint64_t len, uint32_t n_stripes, const uint32_t* masks, uint32_t* bad,
+              hipStream_t s) {
+    ApplyArgs a{};
+    a.in_base = in_base;
+    a.in_stripe = in_stripe;
+    a.in_shard = in_shard;
+    a.out_base = out_base;
+    a.out_stripe = out_stripe;
+    a.out_shard = out_shard;
+    a.len = len;
+    a.n_stripes = n_stripes;
+    a.plans = ps.plans;
+    a.tabs = ps.tabs;
+    a.idx = ps.idx;
+    a.masks = masks;
+    a.lut = ps.lut;
+    a.bad_count = bad;
+    const uint64_t align = uint64_t(reinterpret_cast<uintptr_t>(in_base)) | in_stripe | in_shard |
+                           uint64_t(reinterpret_cast<uintptr_t>(out_base)) | out_stripe | out_shard;
+    const bool aligned = (align % 16) == 0;
+    HEC_HIP(launch_apply(a, int(nin), aligned, launch_config(), s));
+    return HEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Per-device scratch for host-memory calls
+// ---------------------------------------------------------------------------
+static std::mutex g_scratch_mu;
+static std::map<int, std::unique_ptr<Scratch>> g_scratch;
+
+int Scratch::reserve(size_t bytes) {
+    if (bytes <= dcap) return HEC_OK;
+    if (dbuf) HEC_HIP(hipFree(dbuf));
+    dbuf = nullptr;
+    dcap = 0;
+    size_t want = std::max(bytes, size_t(16) << 20);
+    HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dbuf), want));
+    dcap = want;
+    return HEC_OK;
+}
+
+int device_scratch(Scratch** out) {
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    auto it = g_scratch.find(dev);
+    if (it == g_scratch.end()) {
+        std::unique_ptr<Scratch> sc(new Scratch());
+        HEC_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+        it = g_scratch.emplace(dev, std::move(sc)).first;
+    }
+    *out = it->second.get();
+    return HEC_OK;
+}
+
+static uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// upstream check_piece_count!(all) + check_slices!(multi)
+static int check_shards(const hec_rs* rs, const void* shards, const size_t* lens, size_t n_shards) {
+    if (!shards || !lens) return fail(HEC_ERR_INVALID_ARGUMENT, "null shards");
+    if (n_shards < size_t(rs->n)) return HEC_ERR_TOO_FEW_SHARDS;
+    if (n_shards > size_t(rs->n)) return HEC_ERR_TOO_MANY_SHARDS;
+    if (lens[0] == 0) return HEC_ERR_EMPTY_SHARD;
+    for (size_t i = 1; i < n_shards; ++i)
+        if (lens[i] != lens[0]) return HEC_ERR_INCORRECT_SHARD_SIZE;
+    return HEC_OK;
+}
+
+static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* const* parity_out,
+                       std::vector<uint8_t>* parity_vec, size_t L) {
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    Scratch* sc;
+    if ((rc = device_scratch(&sc))) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    const uint64_t Lp = round_up(L, 256);
+    if ((rc = sc->reserve(size_t(Lp) * rs->n))) return rc;
+    for (int i = 0; i < rs->k; ++i)
+        HEC_HIP(hipMemcpyAsync(sc->dbuf + i * Lp, data[i], L, hipMemcpyHostToDevice, sc->stream));
+    uint8_t* par = sc->dbuf + size_t(rs->k) * Lp;
+    if ((rc = run_apply(gd->encode, uint32_t(rs->k), sc->dbuf, 0, Lp, par, 0, Lp, round_up(L, 16), 1,
+                        nullptr, nullptr, sc->stream)))
+        return rc;
+    for (int j = 0; j < rs->m; ++j) {
+        uint8_t* dst = parity_out ? parity_out[j] : parity_vec->data() + size_t(j) * L;
+        HEC_HIP(hipMemcpyAsync(dst, par + j * Lp, L, hipMemcpyDeviceToHost, sc->stream));
+    }
+    HEC_HIP(hipStreamSynchronize(sc->stream));
+    return HEC_OK;
+}
+
+static int reconstruct_host(const hec_rs* rs, uint8_t* const* shards, const size_t* lens,
+                            const uint8_t* present, size_t n_shards, bool data_only) {
+    if (!shards || !lens || !present) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (n_shards < size_t(rs->n)) return HEC_ERR_TOO_FEW_SHARDS;
+    if (n_shards > size_t(rs->n)) return HEC_ERR_TOO_MANY_SHARDS;
+    size_t L = 0;
+    int npresent = 0;
+    for (size_t i = 0; i < n_shards; ++i) {
+        if (!present[i]) continue;
+        if (lens[i] == 0) return HEC_ERR_EMPTY_SHARD;
+        if (npresent && lens[i] != L) return HEC_ERR_INCORRECT_SHARD_SIZE;
+        L = lens[i];
+        ++npresent;
+    }
+    if (npresent == rs->n) return HEC_OK;
+    if (npresent < rs->k) return HEC_ERR_TOO_FEW_SHARDS_PRESENT;
+    Mat coefs;
+    std::vector<uint32_t> in_ids, out_ids;
+    bool noop = false;
+    int rc = decode_plan(rs, present, data_only, coefs, in_ids, out_ids, &noop);
+    if (rc) return rc;
+    for (uint32_t id : out_ids)
+        if (!shards[id]) return fail(HEC_ERR_INVALID_ARGUMENT, "missing shard without a buffer");
+    if (noop) return HEC_OK;
+    Scratch* sc;
+    if ((rc = device_scratch(&sc))) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    const uint64_t Lp = round_up(L, 256);
+    if ((rc = sc->reserve(size_t(Lp) * rs->n))) return rc;
+    HostPlans hp;
+    hp.add(coefs, in_ids, out_ids);
+    if ((rc = sc->adhoc.upload(hp, nullptr, sc->stream))) return rc;
+    for (uint32_t id : in_ids)
+        HEC_HIP(hipMemcpyAsync(sc->dbuf + id * Lp, shards[id], L, hipMemcpyHostToDevice, sc->stream));
+    if ((rc = run_apply(sc->adhoc, uint32_t(rs->k), sc->dbuf, 0, Lp, sc->dbuf, 0, Lp, round_up(L, 16), 1,
+                        nullptr, nullptr, sc->stream)))
+        return rc;
+    for (uint32_t id : out_ids)
+        HEC_HIP(hipMemcpyAsync(shards[id], sc->dbuf + id * Lp, L, hipMemcpyDeviceToHost, sc->stream));
+    HEC_HIP(hipStreamSynchronize(sc->stream));
+    return HEC_OK;
+}
+
+}  // namespace hec
+
+using namespace hec;
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* hec_strerror(int status) {
+    switch (status) {
+        case HEC_OK: return "ok";
+        // reed_solomon_erasure::Error Display texts (upstream 6.0.0)
+        case HEC_ERR_TOO_FEW_SHARDS: return "The number of provided shards is smaller than the one in codec";
+        case HEC_ERR_TOO_MANY_SHARDS: return "The number of provided shards is greater than the one in codec";
+        case HEC_ERR_TOO_FEW_DATA_SHARDS: return "The number of provided data shards is smaller than the one in codec";
+        case HEC_ERR_TOO_MANY_DATA_SHARDS: return "The number of provided data shards is greater than the one in codec";
+        case HEC_ERR_TOO_FEW_PARITY_SHARDS: return "The number of provided parity shards is smaller than the one in codec";
+        case HEC_ERR_TOO_MANY_PARITY_SHARDS: return "The number of provided parity shards is greater than the one in codec";
+        case HEC_ERR_TOO_FEW_BUFFER_SHARDS: return "The number of provided buffer shards is smaller than the number of parity shards in codec";
+        case HEC_ERR_TOO_MANY_BUFFER_SHARDS: return "The number of provided buffer shards is greater than the number of parity shards in codec";
+        case HEC_ERR_INCORRECT_SHARD_SIZE: return "At least one of the provided shards is not of the correct size";
+        case HEC_ERR_TOO_FEW_SHARDS_PRESENT: return "The number of shards present is smaller than number of parity shards, cannot reconstruct missing shards";
+        case HEC_ERR_EMPTY_SHARD: return "The first shard provided is of zero length";
+        case HEC_ERR_INVALID_SHARD_FLAGS: return "The number of flags does not match the total number of shards";
+        case HEC_ERR_INVALID_INDEX: return "The data shard index provided is greater or equal to the number of data shards in codec";
+        // helyim_ec::EcShardError (helyim-ec/src/errors.rs:55-66)
+        case HEC_ERR_IO: return "Io error";
+        case HEC_ERR_UNDERFLOW: return "Only {0} shards found but {0} required";
+        case HEC_ERR_UNEXPECTED_EC_SHARD_SIZE: return "ec shard size expected {0} but actually is {1}";
+        case HEC_ERR_UNEXPECTED_BLOCK_SIZE: return "unexpected block size {0}, buffer size {1}";
+        case HEC_ERR_HIP: return "HIP runtime error";
+        case HEC_ERR_NO_DEVICE: return "no usable GPU device";
+        case HEC_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case HEC_ERR_OUT_OF_MEMORY: return "out of device memory";
+        default: return "unknown status";
+    }
+}
+
+const char* hec_last_error_detail(void) { return g_detail.c_str(); }
+
+const char* hec_version(void) { return "libhec 0.1.0 (gfx950)"; }
+
+int hec_set_launch_config(int vec_per_thread, long max_blocks) {
+    if (vec_per_thread != 1 && vec_per_thread != 2 && vec_per_thread != 4)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "vec_per_thread must be 1, 2 or 4");
+    launch_config().vec_per_thread = vec_per_thread;
+    launch_config().max_blocks = max_blocks < 0 ? 0 : max_blocks;
+    return HEC_OK;
+}
+
+int hec_rs_new(size_t data_shards, size_t parity_shards, hec_rs_t** out) {
+    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    if (data_shards == 0) return HEC_ERR_TOO_FEW_DATA_SHARDS;
+    if (parity_shards == 0) return HEC_ERR_TOO_FEW_PARITY_SHARDS;
+    if (data_shards + parity_shards > 256) return HEC_ERR_TOO_MANY_SHARDS;
+    hec_rs_t* rs = new hec_rs_t();
+    rs->k = int(data_shards);
+    rs->m = int(parity_shards);
+    rs->n = rs->k + rs->m;
+    rs->matrix = build_encoding_matrix(rs->k, rs->n);
+    *out = rs;
+    return HEC_OK;
+}
+
+void hec_rs_free(hec_rs_t* rs) { delete rs; }
+
+size_t hec_rs_data_shard_count(const hec_rs_t* rs) { return rs ? size_t(rs->k) : 0; }
+size_t hec_rs_parity_shard_count(const hec_rs_t* rs) { return rs ? size_t(rs->m) : 0; }
+size_t hec_rs_total_shard_count(const hec_rs_t* rs) { return rs ? size_t(rs->n) : 0; }
+
+int hec_rs_matrix(const hec_rs_t* rs, uint8_t* out, size_t out_len) {
+    if (!rs || !out || out_len < rs->matrix.v.size()) return fail(HEC_ERR_INVALID_ARGUMENT, "bad matrix buffer");
+    std::memcpy(out, rs->matrix.v.data(), rs->matrix.v.size());
+    return HEC_OK;
+}
+
+int hec_rs_encode(const hec_rs_t* rs, uint8_t* const* shards, const size_t* shard_lens, size_t n_shards) {
+    if (!rs) return fail(HEC_ERR_INVALID_ARGUMENT, "null codec");
+    int rc = check_shards(rs, shards, shard_lens, n_shards);
+    if (rc) return rc;
+    return encode_host(rs, const_cast<const uint8_t* const*>(shards), shards + rs->k, nullptr, shard_lens[0]);
+}
+
+int hec_rs_verify(const hec_rs_t* rs, const uint8_t* const* shards, const size_t* shard_lens, size_t n_shards,
+                  int* ok) {
+    if (!rs || !ok) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    int rc = check_shards(rs, shards, shard_lens, n_shards);
+    if (rc) return rc;
+    const size_t L = shard_lens[0];
+    std::vector<uint8_t> par(size_t(rs->m) * L);
+    if ((rc = encode_host(rs, shards, nullptr, &par, L))) return rc;
+    *ok = 1;
+    for (int j = 0; j < rs->m; ++j)
+        if (std::memcmp(par.data() + size_t(j) * L, shards[rs->k + j], L) != 0) *ok = 0;
+    return HEC_OK;
+}
+
+int hec_rs_reconstruct(const hec_rs_t* rs, uint8_t* const* shards, const size_t* shard_lens,
+                       const uint8_t* present, size_t n_shards) {
+    if (!rs) return fail(HEC_ERR_INVALID_ARGUMENT, "null codec");
+    return reconstruct_host(rs, shards, shard_lens, present, n_shards, false);
+}
+
+int hec_rs_reconstruct_data(const hec_rs_t* rs, uint8_t* const* shards, const size_t* shard_lens,
+                            const uint8_t* present, size_t n_shards) {
+    if (!rs) return fail(HEC_ERR_INVALID_ARGUMENT, "null codec");
+    return reconstruct_host(rs, shards, shard_lens, present, n_shards, true);
+}
+
+int hec_gpu_encode_batch(const hec_rs_t* rs, const uint8_t* d_data, uint64_t data_stripe_stride,
+                         uint64_t data_shard_stride, uint8_t* d_parity, uint64_t parity_stripe_stride,
+                         uint64_t parity_shard_stride, uint64_t shard_len, uint32_t n_stripes, void* stream) {
+    if (!rs || !d_data || !d_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    return run_apply(gd->encode, uint32_t(rs->k), d_data, data_stripe_stride, data_shard_stride, d_parity,
+                     parity_stripe_stride, parity_shard_stride, shard_len, n_stripes, nullptr, nullptr,
+                     static_cast<hipStream_t>(stream));
+}
+
+int hec_gpu_reconstruct_batch(const hec_rs_t* rs, uint8_t* d_shards, uint64_t stripe_stride, uint64_t shard_stride,
+                              uint64_t shard_len, uint32_t n_stripes, const uint32_t* d_present_masks,
+                              uint32_t* d_bad_stripes, void* stream) {
+    if (!rs || !d_shards || !d_present_masks) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if ((rc = ensure_dense_decode(rs, gd, s))) return rc;
+    return run_apply(gd->decode_dense, uint32_t(rs->k), d_shards, stripe_stride, shard_stride, d_shards,
+                     stripe_stride, shard_stride, shard_len, n_stripes, d_present_masks, d_bad_stripes, s);
+}
+
+int hec_gpu_fill_splitmix(uint8_t* d_base, uint64_t stripe_stride, uint64_t bytes_per_stripe, uint32_t n_stripes,
+                          uint64_t seed_base, void* stream) {
+    if (!d_base) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    HEC_HIP(launch_fill_splitmix(d_base, stripe_stride, bytes_per_stripe, n_stripes, seed_base,
+                                 static_cast<hipStream_t>(stream)));
+    return HEC_OK;
+}
+
+}  // extern "C"

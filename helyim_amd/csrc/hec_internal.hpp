@@ -1,0 +1,90 @@
+// Internal declarations shared by the C ABI (hec_api.cpp) and the file layer
+// (ec_files.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hec.h"
+#include "gf256.hpp"
+#include "rs_kernels.hpp"
+
+struct hec_rs {
+    int k = 0, m = 0, n = 0;
+    hec::Mat matrix;  // n x k
+};
+
+namespace hec {
+
+// Thread-local failure detail (hec_last_error_detail).
+void set_detail(const std::string& s);
+int fail(int code, const std::string& detail);
+int hip_fail(hipError_t e, const char* what);
+
+#define HEC_HIP(call)                                          \
+    do {                                                       \
+        hipError_t e_ = (call);                                \
+        if (e_ != hipSuccess) return ::hec::hip_fail(e_, #call); \
+    } while (0)
+
+// Host-side plan list, uploaded as one DevicePlanSet.
+struct HostPlans {
+    std::vector<DevPlan> plans;
+    std::vector<uint32_t> tabs;
+    std::vector<uint32_t> idx;
+    // Append a plan: out rows = coefs (nout x nin) over inputs in_ids.
+    uint32_t add(const Mat& coefs, const std::vector<uint32_t>& in_ids,
+                 const std::vector<uint32_t>& out_ids);
+    uint32_t add_noop(uint32_t nin);
+};
+
+// Device copy of a HostPlans (+ optional mask LUT).
+struct DevicePlanSet {
+    DevPlan* plans = nullptr;
+    uint32_t* tabs = nullptr;
+    uint32_t* idx = nullptr;
+    uint32_t* lut = nullptr;
+    size_t cap_plans = 0, cap_tabs = 0, cap_idx = 0, cap_lut = 0;
+    int upload(const HostPlans& hp, const std::vector<uint32_t>* lut_host, hipStream_t s);
+    void release();
+};
+
+// Decode plan of one erasure pattern (upstream reconstruct semantics).
+// present: n flags. data_only: skip missing parity. Returns HEC_OK or
+// TOO_FEW_SHARDS_PRESENT; *noop = true when every shard is present.
+int decode_plan(const hec_rs* rs, const uint8_t* present, bool data_only, Mat& coefs,
+                std::vector<uint32_t>& in_ids, std::vector<uint32_t>& out_ids, bool* noop);
+
+// Per-device state shared by all contexts of one geometry.
+struct GeomDevice {
+    DevicePlanSet encode;        // plan 0 = encode
+    DevicePlanSet decode_dense;  // LUT over all 2^n present masks (n <= 16)
+    bool decode_ready = false;
+};
+int geom_device(const hec_rs* rs, GeomDevice** out);
+int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s);
+
+LaunchConfig& launch_config();
+int current_device(int* dev);
+
+// Per-device scratch for host-memory entry points (serialised by mu).
+struct Scratch {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    uint8_t* dbuf = nullptr;
+    size_t dcap = 0;
+    DevicePlanSet adhoc;
+    int reserve(size_t bytes);
+};
+int device_scratch(Scratch** out);
+
+// Run one plan set over a strided batch (plan 0 for every stripe unless masks).
+int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uint64_t in_stripe,
+              uint64_t in_shard, uint8_t* out_base, uint64_t out_stripe, uint64_t out_shard,
+              uint64_t len, uint32_t n_stripes, const uint32_t* masks, uint32_t* bad,
+              hipStream_t s);
+
+}  // namespace hec

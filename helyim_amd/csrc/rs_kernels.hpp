@@ -1,0 +1,59 @@
+// Shared host/device declarations for the gfx950 RS kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace hec {
+
+// One coding plan: nout output rows = coefficient matrix (nout x nin) applied
+// to the nin input shards of a stripe. Encode is one plan (inputs = data
+// shards, outputs = parity shards); decode has one plan per erasure pattern
+// (inputs = first nin present shards, outputs = erased shards), matching
+// upstream reconstruct's "first data_shard_count present shards" rule.
+struct DevPlan {
+    uint32_t nin;      // inputs (== data shard count)
+    uint32_t nout;     // outputs; 0 = nothing to do (all shards present)
+    uint32_t tab_off;  // word offset of this plan's tables: [nin][nout][kTabWords]
+    uint32_t idx_off;  // word offset of [nin] input shard ids then [nout] output ids
+};
+
+constexpr uint32_t kNoPlan = 0xFFFFFFFFu;   // mask LUT entry: too few shards present
+constexpr int kThreads = 256;               // 4 waves of 64 lanes
+constexpr int kVecBytes = 16;               // one dwordx4 per lane per access
+
+struct ApplyArgs {
+    const uint8_t* in_base;      // input shard (stripe s, id i) = in_base + s*in_stripe + i*in_shard
+    uint64_t in_stripe;
+    uint64_t in_shard;
+    uint8_t* out_base;           // output shard (stripe s, id j) = out_base + s*out_stripe + j*out_shard
+    uint64_t out_stripe;
+    uint64_t out_shard;
+    uint64_t len;                // shard length in bytes (same for every stripe of the batch)
+    uint64_t n_items;            // n_stripes * chunks_per_stripe
+    uint32_t chunks_per_stripe;  // ceil(len / chunk_bytes)
+    uint32_t n_stripes;
+    const DevPlan* plans;
+    const uint32_t* tabs;
+    const uint32_t* idx;
+    const uint32_t* masks;       // optional per-stripe present mask (bit i = shard i present)
+    const uint32_t* lut;         // mask -> plan id (used when masks != nullptr)
+    uint32_t* bad_count;         // optional: stripes skipped for too few present shards
+};
+
+struct LaunchConfig {
+    int vec_per_thread = 2;      // 16-byte vectors per lane per chunk (1, 2 or 4)
+    long max_blocks = 0;         // grid cap (0 = one block per chunk)
+};
+
+// Launch one coding pass. k_fixed: number of inputs the caller guarantees
+// (10 selects the unrolled helyim RS(10,4) path; anything else the generic loop).
+hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
+                        hipStream_t stream);
+
+// splitmix64 byte stream per stripe (bench/test data generator):
+// stripe s: bytes_per_stripe bytes at base + s*stripe_stride, word n (n>=1) =
+// mix(seed_base + s + n*gamma), little endian.
+hipError_t launch_fill_splitmix(uint8_t* base, uint64_t stripe_stride, uint64_t bytes_per_stripe,
+                                uint32_t n_stripes, uint64_t seed_base, hipStream_t stream);
+
+}  // namespace hec

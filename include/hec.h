@@ -1,0 +1,170 @@
+/*
+ * hec.h -- C ABI of the MI355X-native RS(10,4) erasure-coding engine that
+ * replaces helyim-ec's CPU path (libhec.so, built for gfx950).
+ *
+ * Every entry point takes plain pointers and sizes. Each one names the
+ * reference interface it replaces (paths relative to /root/reference):
+ *
+ *  - the arithmetic boundary: reed_solomon_erasure::ReedSolomon<galois_8::Field>
+ *    {new, encode, reconstruct} as called at helyim-ec/src/encoder.rs:191,
+ *    208-209, 249-250, 288 and helyim-store/src/erasure_coding/mod.rs:411-412,
+ *    426 (crate 6.0.0, git helyim/reed-solomon-erasure, Cargo.toml:72);
+ *  - the crate API boundary: helyim_ec::write_ec_files / rebuild_ec_files
+ *    (helyim-ec/src/encoder.rs:39-50, exported at helyim-ec/src/lib.rs:17),
+ *    called by helyim-store/src/server.rs:468 and :497.
+ *
+ * All compute runs on the GPU through HIP kernels. There is no CPU fallback:
+ * without a usable GPU every compute entry point returns HEC_ERR_NO_DEVICE or
+ * HEC_ERR_HIP.
+ *
+ * Threading: a hec_rs_t is immutable after hec_rs_new and may be shared by
+ * threads (upstream ReedSolomon is Send + Sync). Device state (tables,
+ * decode-pattern cache, staging buffers) is per device and mutex guarded.
+ * Host-memory entry points synchronise before returning; the hec_gpu_*
+ * batch entry points are asynchronous on the caller's stream.
+ */
+#ifndef HEC_H
+#define HEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------
+ * 1..13 are 1:1 with reed_solomon_erasure::Error (declaration order);
+ * 32..35 with helyim_ec::EcShardError (helyim-ec/src/errors.rs:55-66);
+ * 64.. are device / argument errors of this library. */
+enum hec_status {
+    HEC_OK = 0,
+    HEC_ERR_TOO_FEW_SHARDS = 1,
+    HEC_ERR_TOO_MANY_SHARDS = 2,
+    HEC_ERR_TOO_FEW_DATA_SHARDS = 3,
+    HEC_ERR_TOO_MANY_DATA_SHARDS = 4,
+    HEC_ERR_TOO_FEW_PARITY_SHARDS = 5,
+    HEC_ERR_TOO_MANY_PARITY_SHARDS = 6,
+    HEC_ERR_TOO_FEW_BUFFER_SHARDS = 7,
+    HEC_ERR_TOO_MANY_BUFFER_SHARDS = 8,
+    HEC_ERR_INCORRECT_SHARD_SIZE = 9,
+    HEC_ERR_TOO_FEW_SHARDS_PRESENT = 10,
+    HEC_ERR_EMPTY_SHARD = 11,
+    HEC_ERR_INVALID_SHARD_FLAGS = 12,
+    HEC_ERR_INVALID_INDEX = 13,
+    HEC_ERR_IO = 32,                      /* EcShardError::Io */
+    HEC_ERR_UNDERFLOW = 33,               /* EcShardError::Underflow */
+    HEC_ERR_UNEXPECTED_EC_SHARD_SIZE = 34,/* EcShardError::UnexpectedEcShardSize */
+    HEC_ERR_UNEXPECTED_BLOCK_SIZE = 35,   /* EcShardError::UnexpectedBlockSize */
+    HEC_ERR_HIP = 64,                     /* a HIP runtime call failed */
+    HEC_ERR_NO_DEVICE = 65,               /* no usable GPU */
+    HEC_ERR_INVALID_ARGUMENT = 66,        /* null pointer, bad stride, ... */
+    HEC_ERR_OUT_OF_MEMORY = 67
+};
+
+/* Static text for a status code (the upstream Display string where one exists). */
+const char* hec_strerror(int status);
+/* Thread-local detail of the last failure on this thread (e.g. the errno text,
+ * the two sizes of UnexpectedEcShardSize). Empty string when none. */
+const char* hec_last_error_detail(void);
+
+/* ---- geometry constants (helyim-ec/src/lib.rs:46-50) ---------------------- */
+#define HEC_DATA_SHARDS_COUNT 10u
+#define HEC_PARITY_SHARDS_COUNT 4u
+#define HEC_TOTAL_SHARDS_COUNT 14u
+#define HEC_LARGE_BLOCK_SIZE (1024ull * 1024ull * 1024ull)
+#define HEC_SMALL_BLOCK_SIZE (1024ull * 1024ull)
+
+/* ---- codec context: replaces ReedSolomon<galois_8::Field> ----------------- */
+typedef struct hec_rs hec_rs_t;
+
+/* ReedSolomon::new(data_shards, parity_shards) (encoder.rs:208-209).
+ * Errors: TOO_FEW_DATA_SHARDS (0 data), TOO_FEW_PARITY_SHARDS (0 parity),
+ * TOO_MANY_SHARDS (data + parity > 256). */
+int hec_rs_new(size_t data_shards, size_t parity_shards, hec_rs_t** out);
+void hec_rs_free(hec_rs_t* rs);
+size_t hec_rs_data_shard_count(const hec_rs_t* rs);
+size_t hec_rs_parity_shard_count(const hec_rs_t* rs);
+size_t hec_rs_total_shard_count(const hec_rs_t* rs);
+/* Copies the (total x data) row-major encoding matrix into out. */
+int hec_rs_matrix(const hec_rs_t* rs, uint8_t* out, size_t out_len);
+
+/* ReedSolomon::encode(&mut shards) (encoder.rs:191), host memory.
+ * shards[0..data) are read, shards[data..total) receive parity in place.
+ * shard_lens[i] is the length of shards[i]. Errors: TOO_FEW_SHARDS /
+ * TOO_MANY_SHARDS (n_shards != total), EMPTY_SHARD, INCORRECT_SHARD_SIZE. */
+int hec_rs_encode(const hec_rs_t* rs, uint8_t* const* shards, const size_t* shard_lens,
+                  size_t n_shards);
+
+/* ReedSolomon::verify(&shards): *ok = 1 when the parity matches the data. */
+int hec_rs_verify(const hec_rs_t* rs, const uint8_t* const* shards, const size_t* shard_lens,
+                  size_t n_shards, int* ok);
+
+/* ReedSolomon::reconstruct(&mut [Option<Vec<u8>>]) (encoder.rs:288,
+ * erasure_coding/mod.rs:426). present[i] != 0 marks Some(shard); shard_lens
+ * of absent slots are ignored. Absent slots must point at a caller buffer of
+ * the common shard length (upstream allocates vec![0; len]); they are filled.
+ * All present -> no-op. Errors: TOO_FEW_SHARDS / TOO_MANY_SHARDS,
+ * EMPTY_SHARD, INCORRECT_SHARD_SIZE, TOO_FEW_SHARDS_PRESENT. Decode uses the
+ * first data_shards present shards in index order, as upstream does. */
+int hec_rs_reconstruct(const hec_rs_t* rs, uint8_t* const* shards, const size_t* shard_lens,
+                       const uint8_t* present, size_t n_shards);
+/* ReedSolomon::reconstruct_data: as above but absent parity slots are left
+ * untouched. */
+int hec_rs_reconstruct_data(const hec_rs_t* rs, uint8_t* const* shards, const size_t* shard_lens,
+                            const uint8_t* present, size_t n_shards);
+
+/* ---- device-resident batches (no reference counterpart: the GPU form of the
+ * encode_data_one_batch loop, encoder.rs:158-198, over many stripes) -------
+ * Shard (stripe s, shard i) lives at base + s*stripe_stride + i*shard_stride.
+ * Pointers are device pointers on the current HIP device; stream is a
+ * hipStream_t (NULL = default stream). Calls are asynchronous. */
+
+/* Encode n_stripes stripes: read data shards 0..data from d_data, write parity
+ * shards 0..parity to d_parity (shard index relative to each base). */
+int hec_gpu_encode_batch(const hec_rs_t* rs,
+                         const uint8_t* d_data, uint64_t data_stripe_stride, uint64_t data_shard_stride,
+                         uint8_t* d_parity, uint64_t parity_stripe_stride, uint64_t parity_shard_stride,
+                         uint64_t shard_len, uint32_t n_stripes, void* stream);
+
+/* Reconstruct n_stripes stripes of all total shards in place. d_present_masks
+ * (device, n_stripes words): bit i set = shard i present. Stripes with every
+ * shard present are left untouched (upstream no-op); stripes with fewer than
+ * data_shards present are skipped and counted into *d_bad_stripes (device
+ * word, optional, accumulated). Requires total shards <= 16. */
+int hec_gpu_reconstruct_batch(const hec_rs_t* rs, uint8_t* d_shards, uint64_t stripe_stride,
+                              uint64_t shard_stride, uint64_t shard_len, uint32_t n_stripes,
+                              const uint32_t* d_present_masks, uint32_t* d_bad_stripes,
+                              void* stream);
+
+/* Deterministic splitmix64 stripe data (bench / test inputs): stripe s gets
+ * bytes_per_stripe bytes at d_base + s*stripe_stride, 64-bit word n (n >= 1)
+ * = splitmix64_mix(seed_base + s + n * 0x9E3779B97F4A7C15), little endian. */
+int hec_gpu_fill_splitmix(uint8_t* d_base, uint64_t stripe_stride, uint64_t bytes_per_stripe,
+                          uint32_t n_stripes, uint64_t seed_base, void* stream);
+
+/* ---- file level: helyim_ec::write_ec_files / rebuild_ec_files ------------ */
+
+/* write_ec_files(base_filename) (encoder.rs:39-46): base.dat -> base.ec00..ec13. */
+int hec_write_ec_files(const char* base_filename);
+/* generate_ec_files(base, buf_size, large_block_size, small_block_size)
+ * (encoder.rs:52-71): same, with explicit geometry (tests use small blocks to
+ * exercise the large-row path). */
+int hec_write_ec_files_ex(const char* base_filename, uint64_t buf_size, uint64_t large_block_size,
+                          uint64_t small_block_size);
+/* rebuild_ec_files(base_filename) -> Vec<u32> (encoder.rs:48-50, 73-109,
+ * 244-307): recreates every missing .ecNN. rebuilt_ids (capacity 14) receives
+ * the rebuilt shard ids in ascending order, *n_rebuilt their count. */
+int hec_rebuild_ec_files(const char* base_filename, uint32_t* rebuilt_ids, size_t* n_rebuilt);
+
+/* ---- tuning / introspection ----------------------------------------------- */
+/* Kernel launch configuration: 16-byte vectors per lane per chunk (1, 2, 4)
+ * and grid cap (0 = one workgroup per chunk). Returns previous values. */
+int hec_set_launch_config(int vec_per_thread, long max_blocks);
+/* Version string of the library build. */
+const char* hec_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HEC_H */

@@ -1,0 +1,248 @@
+/*
+ * CPU oracle for the helyim-ec RS(10,4) hot path -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Independent plain-C restatement of the arithmetic behind helyim-ec
+ * (/root/reference/helyim-ec/src/encoder.rs:191,208-209,249-250,288), which
+ * lives in the un-vendored crate reed-solomon-erasure 6.0.0 (git
+ * helyim/reed-solomon-erasure, branch main, feature simd-accel;
+ * /root/reference/Cargo.toml:72). Used by tests/ (bit-exact checker on the GPU
+ * box) and by bench.py's cpu_baseline leg (the timed CPU path, kind "port").
+ * Never linked into or called by the product library helyim_amd/libhec.so.
+ *
+ * Two encode kernels, selected by the caller:
+ *   simd = 0 : scalar 256x256 MUL_TABLE lookups (upstream's non-SIMD path)
+ *   simd = 1 : AVX2 16-entry low/high nibble product tables + vpshufb, the
+ *              same algorithm class as upstream simd_c/reedsolomon.c
+ *              (reedsolomon_gal_mul / reedsolomon_gal_mul_xor).
+ * Loop order follows upstream code_some_slices: input-major, each output
+ * slice mul (first input) or mul-xor (later inputs) over the whole slice.
+ *
+ * Pinned by tests/golden/upstream_kat.json and cross-checked against
+ * oracle/rs_oracle.py on the fixtures under tests/golden/.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <immintrin.h>
+
+static uint8_t EXP[510];
+static int LOG[256];
+static uint8_t MUL[256][256];
+static int g_init = 0;
+
+static void init_tables(void) {
+    if (g_init) return;
+    int x = 1;
+    for (int i = 0; i < 255; i++) {
+        EXP[i] = (uint8_t)x;
+        LOG[x] = i;
+        x <<= 1;
+        if (x & 0x100) x ^= 0x11D;
+    }
+    for (int i = 255; i < 510; i++) EXP[i] = EXP[i - 255];
+    for (int a = 0; a < 256; a++)
+        for (int b = 0; b < 256; b++)
+            MUL[a][b] = (a && b) ? EXP[LOG[a] + LOG[b]] : 0;
+    g_init = 1;
+}
+
+uint8_t orc_gf_mul(uint8_t a, uint8_t b) { init_tables(); return MUL[a][b]; }
+
+uint8_t orc_gf_exp(uint8_t a, unsigned n) {
+    init_tables();
+    if (n == 0) return 1;
+    if (a == 0) return 0;
+    return EXP[(LOG[a] * (unsigned long)n) % 255];
+}
+
+static uint8_t gf_inv(uint8_t a) { return EXP[(255 - LOG[a]) % 255]; }
+
+/* Gauss-Jordan over GF(2^8); returns 0 on success, -1 if singular. */
+static int invert(const uint8_t* m, uint8_t* out, int n) {
+    uint8_t* w = (uint8_t*)malloc((size_t)n * 2 * n);
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < 2 * n; c++)
+            w[r * 2 * n + c] = c < n ? m[r * n + c] : (uint8_t)(c - n == r);
+    for (int r = 0; r < n; r++) {
+        uint8_t* row = w + r * 2 * n;
+        if (row[r] == 0) {
+            for (int b = r + 1; b < n; b++) {
+                uint8_t* rb = w + b * 2 * n;
+                if (rb[r]) {
+                    for (int c = 0; c < 2 * n; c++) { uint8_t t = row[c]; row[c] = rb[c]; rb[c] = t; }
+                    break;
+                }
+            }
+        }
+        if (row[r] == 0) { free(w); return -1; }
+        if (row[r] != 1) {
+            uint8_t s = gf_inv(row[r]);
+            for (int c = 0; c < 2 * n; c++) row[c] = MUL[s][row[c]];
+        }
+        for (int o = 0; o < n; o++) {
+            if (o == r) continue;
+            uint8_t* ro = w + o * 2 * n;
+            uint8_t f = ro[r];
+            if (f) for (int c = 0; c < 2 * n; c++) ro[c] ^= MUL[f][row[c]];
+        }
+    }
+    for (int r = 0; r < n; r++) memcpy(out + r * n, w + r * 2 * n + n, n);
+    free(w);
+    return 0;
+}
+
+typedef struct {
+    int k, m, n;
+    uint8_t* matrix; /* n x k */
+} orc_rs;
+
+void* orc_rs_new(int k, int m) {
+    init_tables();
+    if (k <= 0 || m <= 0 || k + m > 256) return NULL;
+    orc_rs* rs = (orc_rs*)calloc(1, sizeof(orc_rs));
+    rs->k = k; rs->m = m; rs->n = k + m;
+    int n = k + m;
+    uint8_t* v = (uint8_t*)malloc((size_t)n * k);
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < k; c++) v[r * k + c] = orc_gf_exp((uint8_t)r, (unsigned)c);
+    uint8_t* inv = (uint8_t*)malloc((size_t)k * k);
+    invert(v, inv, k);
+    rs->matrix = (uint8_t*)malloc((size_t)n * k);
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < k; c++) {
+            uint8_t acc = 0;
+            for (int t = 0; t < k; t++) acc ^= MUL[v[r * k + t]][inv[t * k + c]];
+            rs->matrix[r * k + c] = acc;
+        }
+    free(v); free(inv);
+    return rs;
+}
+
+void orc_rs_free(void* p) {
+    orc_rs* rs = (orc_rs*)p;
+    if (!rs) return;
+    free(rs->matrix);
+    free(rs);
+}
+
+void orc_rs_matrix(void* p, uint8_t* out) {
+    orc_rs* rs = (orc_rs*)p;
+    memcpy(out, rs->matrix, (size_t)rs->n * rs->k);
+}
+
+int orc_invert(const uint8_t* m, uint8_t* out, int n) { init_tables(); return invert(m, out, n); }
+
+/* ---- slice kernels -------------------------------------------------------- */
+static void mul_slice_scalar(uint8_t c, const uint8_t* in, uint8_t* out, size_t len, int do_xor) {
+    const uint8_t* t = MUL[c];
+    if (do_xor) for (size_t i = 0; i < len; i++) out[i] ^= t[in[i]];
+    else        for (size_t i = 0; i < len; i++) out[i] = t[in[i]];
+}
+
+__attribute__((target("avx2")))
+static void mul_slice_avx2(uint8_t c, const uint8_t* in, uint8_t* out, size_t len, int do_xor) {
+    uint8_t lo[16], hi[16];
+    for (int x = 0; x < 16; x++) { lo[x] = MUL[c][x]; hi[x] = MUL[c][x << 4]; }
+    const __m256i tlo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)lo));
+    const __m256i thi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)hi));
+    const __m256i mask = _mm256_set1_epi8(0x0f);
+    size_t i = 0;
+    for (; i + 32 <= len; i += 32) {
+        __m256i v = _mm256_loadu_si256((const __m256i*)(in + i));
+        __m256i l = _mm256_and_si256(v, mask);
+        __m256i h = _mm256_and_si256(_mm256_srli_epi64(v, 4), mask);
+        __m256i p = _mm256_xor_si256(_mm256_shuffle_epi8(tlo, l), _mm256_shuffle_epi8(thi, h));
+        if (do_xor) p = _mm256_xor_si256(p, _mm256_loadu_si256((const __m256i*)(out + i)));
+        _mm256_storeu_si256((__m256i*)(out + i), p);
+    }
+    if (i < len) mul_slice_scalar(c, in + i, out + i, len - i, do_xor);
+}
+
+static int g_have_avx2 = -1;
+static int have_avx2(void) {
+    if (g_have_avx2 < 0) g_have_avx2 = __builtin_cpu_supports("avx2") ? 1 : 0;
+    return g_have_avx2;
+}
+
+int orc_have_avx2(void) { return have_avx2(); }
+
+/* out[r] = XOR_i coefs[r*ncols + i] * in[i], upstream code_some_slices order. */
+void orc_code_some_slices(const uint8_t* coefs, int nrows, int ninputs,
+                          const uint8_t* const* in, uint8_t* const* out, size_t len, int simd) {
+    init_tables();
+    int use_avx = simd && have_avx2();
+    for (int i = 0; i < ninputs; i++)
+        for (int r = 0; r < nrows; r++) {
+            uint8_t c = coefs[r * ninputs + i];
+            if (use_avx) mul_slice_avx2(c, in[i], out[r], len, i != 0);
+            else         mul_slice_scalar(c, in[i], out[r], len, i != 0);
+        }
+}
+
+/* encode: shards[0..k) data, shards[k..n) parity written in place. */
+void orc_encode(void* p, uint8_t* const* shards, size_t len, int simd) {
+    orc_rs* rs = (orc_rs*)p;
+    orc_code_some_slices(rs->matrix + (size_t)rs->k * rs->k, rs->m, rs->k,
+                         (const uint8_t* const*)shards, shards + rs->k, len, simd);
+}
+
+/* reconstruct (upstream semantics): present[i] != 0 marks valid shards; every
+ * missing slot must point to a caller buffer of len bytes (upstream allocates
+ * vec![0; len]). Returns 0, or -1 if fewer than k shards are present.
+ * data_only = 1 mirrors reconstruct_data (missing parity untouched). */
+int orc_reconstruct(void* p, uint8_t* const* shards, const uint8_t* present, size_t len,
+                    int data_only, int simd) {
+    orc_rs* rs = (orc_rs*)p;
+    int k = rs->k, n = rs->n;
+    int npresent = 0;
+    for (int i = 0; i < n; i++) npresent += present[i] ? 1 : 0;
+    if (npresent == n) return 0;
+    if (npresent < k) return -1;
+    int valid[256], invalid[256], nv = 0, ni = 0;
+    const uint8_t* sub[256];
+    for (int i = 0; i < n; i++) {
+        if (present[i]) { if (nv < k) { sub[nv] = shards[i]; valid[nv++] = i; } }
+        else invalid[ni++] = i;
+    }
+    uint8_t* a = (uint8_t*)malloc((size_t)k * k);
+    uint8_t* inv = (uint8_t*)malloc((size_t)k * k);
+    for (int r = 0; r < k; r++) memcpy(a + r * k, rs->matrix + (size_t)valid[r] * k, k);
+    invert(a, inv, k);
+    uint8_t* rows = (uint8_t*)malloc((size_t)n * k);
+    uint8_t* outs[256];
+    int nr = 0;
+    for (int t = 0; t < ni; t++)
+        if (invalid[t] < k) {
+            memset(shards[invalid[t]], 0, len);
+            memcpy(rows + nr * k, inv + (size_t)invalid[t] * k, k);
+            outs[nr++] = shards[invalid[t]];
+        }
+    if (nr) orc_code_some_slices(rows, nr, k, sub, outs, len, simd);
+    if (!data_only) {
+        nr = 0;
+        for (int t = 0; t < ni; t++)
+            if (invalid[t] >= k) {
+                memcpy(rows + nr * k, rs->matrix + (size_t)invalid[t] * k, k);
+                outs[nr++] = shards[invalid[t]];
+            }
+        if (nr) orc_code_some_slices(rows, nr, k, (const uint8_t* const*)shards, outs, len, simd);
+    }
+    free(a); free(inv); free(rows);
+    return 0;
+}
+
+/* splitmix64 byte stream: word n (n >= 1) = mix(seed + n*gamma), little endian. */
+void orc_splitmix64_fill(uint64_t seed, uint8_t* out, size_t nbytes) {
+    size_t nw = nbytes / 8;
+    for (size_t w = 0; w < nw + 1; w++) {
+        uint64_t z = seed + (uint64_t)(w + 1) * 0x9E3779B97F4A7C15ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        z ^= z >> 31;
+        for (int b = 0; b < 8; b++) {
+            size_t o = w * 8 + b;
+            if (o >= nbytes) return;
+            out[o] = (uint8_t)(z >> (8 * b));
+        }
+    }
+}

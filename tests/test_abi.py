@@ -1,0 +1,109 @@
+"""The drop-in boundary without a GPU: libhec loads, exports every symbol the
+header declares, and its host-side logic (geometry, matrix, argument/error
+checks that precede any device work) behaves like upstream."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, has_gpu
+
+HEADER = os.path.join(ROOT, "include", "hec.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hec_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_header():
+    import helyim_amd
+    from helyim_amd import _lib
+    names = declared_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(helyim_amd.lib, n), n
+        assert n in _lib.SIGNATURES, n
+    assert "gfx950" in helyim_amd.version()
+
+
+def test_library_is_gfx950_code_object():
+    so = os.path.join(ROOT, "helyim_amd", "libhec.so")
+    blob = open(so, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_status_codes_and_strings():
+    from helyim_amd import _lib, errors
+    assert _lib.strerror(0) == "ok"
+    assert "smaller than number of parity shards" in _lib.strerror(errors.TooFewShardsPresent.code)
+    assert "ec shard size expected" in _lib.strerror(errors.UnexpectedEcShardSize.code)
+
+
+def test_rs_new_errors():
+    import helyim_amd as H
+    with pytest.raises(H.TooFewDataShards):
+        H.ReedSolomon(0, 4)
+    with pytest.raises(H.TooFewParityShards):
+        H.ReedSolomon(10, 0)
+    with pytest.raises(H.TooManyShards):
+        H.ReedSolomon(250, 7)
+    rs = H.ReedSolomon(128, 128)
+    assert rs.total_shard_count() == 256
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (3, 2), (17, 3), (1, 1), (200, 56)])
+def test_matrix_matches_oracle(k, m):
+    import helyim_amd as H
+    from oracle import rs_oracle as O
+    assert np.array_equal(H.ReedSolomon(k, m).matrix(), O.build_matrix(k, k + m))
+
+
+def test_argument_errors_before_device():
+    import helyim_amd as H
+    rs = H.ReedSolomon(10, 4)
+    L = 64
+    sh = [np.zeros(L, np.uint8) for _ in range(14)]
+    with pytest.raises(H.TooFewShards):
+        rs.encode(sh[:13])
+    with pytest.raises(H.TooManyShards):
+        rs.encode(sh + [np.zeros(L, np.uint8)])
+    with pytest.raises(H.EmptyShard):
+        rs.encode([np.zeros(0, np.uint8)] + sh[1:])
+    with pytest.raises(H.IncorrectShardSize):
+        rs.encode(sh[:13] + [np.zeros(L + 1, np.uint8)])
+    with pytest.raises(H.TooFewShardsPresent):
+        rs.reconstruct([None] * 5 + sh[5:])
+    with pytest.raises(H.IncorrectShardSize):
+        rs.reconstruct([None] + sh[1:13] + [np.zeros(3, np.uint8)])
+    with pytest.raises(H.TooFewShards):
+        rs.reconstruct(sh[:12])
+    # all present: upstream no-op, no device work
+    rs.reconstruct(list(sh))
+
+
+@pytest.mark.skipif(has_gpu(), reason="checks the no-GPU error path")
+def test_no_cpu_fallback():
+    import helyim_amd as H
+    rs = H.ReedSolomon(10, 4)
+    sh = [np.ones(64, np.uint8) for _ in range(14)]
+    with pytest.raises(H.DeviceError) as ei:
+        rs.encode(sh)
+    assert ei.value.code == 65  # HEC_ERR_NO_DEVICE
+
+
+def test_constants_and_ext():
+    import helyim_amd as H
+    assert (H.DATA_SHARDS_COUNT, H.PARITY_SHARDS_COUNT, H.TOTAL_SHARDS_COUNT) == (10, 4, 14)
+    assert H.ERASURE_CODING_LARGE_BLOCK_SIZE == 1 << 30
+    assert H.ERASURE_CODING_SMALL_BLOCK_SIZE == 1 << 20
+    assert [H.to_ext(i) for i in (0, 9, 13)] == [".ec00", ".ec09", ".ec13"]
+
+
+def test_file_layer_io_errors(tmp_path):
+    import helyim_amd as H
+    with pytest.raises(H.Io):
+        H.write_ec_files(str(tmp_path / "missing"))

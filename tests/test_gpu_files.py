@@ -1,0 +1,96 @@
+"""File-level drop-ins (write_ec_files / rebuild_ec_files) on the GPU against
+the committed 30 MB fixture and the oracle's encoder.rs restatement."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import rs_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _sha(path):
+    return O.sha256(open(path, "rb").read())
+
+
+def test_volume_30mb_encode_rebuild(gpu, golden, tmp_path):
+    import helyim_amd as H
+    g = golden("volume_30mb.json")
+    base = str(tmp_path / "1")
+    vol = O.synthetic_volume(g["dat_bytes"])
+    open(base + ".dat", "wb").write(vol.tobytes())
+    H.write_ec_files(base)
+    assert [_sha(base + H.to_ext(i)) for i in range(14)] == g["shard_sha256"]
+    for drop in g["drops"]:
+        for i in drop:
+            os.remove(base + H.to_ext(i))
+        assert H.rebuild_ec_files(base) == sorted(drop)
+        assert [_sha(base + H.to_ext(i)) for i in range(14)] == g["shard_sha256"]
+    assert H.rebuild_ec_files(base) == []
+
+
+@pytest.mark.parametrize("size", [1, 639, 640, 641, 2000, 6401, 6400 * 2 + 3, 6400 * 3])
+def test_small_geometry_vs_oracle(gpu, tmp_path, size):
+    """Large-row path exercised with 640-byte 'large' and 32-byte 'small' blocks."""
+    import helyim_amd as H
+    buf, large, small = 16, 640, 32
+    dat = O.splitmix64_bytes(5 + size, size).tobytes()
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    for base in (a, b):
+        open(base + ".dat", "wb").write(dat)
+    H.generate_ec_files(a, buf, large, small)
+    O.write_ec_files(b, buf, large, small)
+    for i in range(14):
+        assert open(a + H.to_ext(i), "rb").read() == open(b + O.to_ext(i), "rb").read(), i
+
+
+def test_unexpected_block_size(gpu, tmp_path):
+    import helyim_amd as H
+    base = str(tmp_path / "v")
+    open(base + ".dat", "wb").write(b"x" * 100)
+    with pytest.raises(H.UnexpectedBlockSize):
+        H.generate_ec_files(base, 24, 640, 32)
+
+
+def test_rebuild_errors(gpu, tmp_path):
+    import helyim_amd as H
+    base = str(tmp_path / "v")
+    vol = O.synthetic_volume(3_000_000)
+    open(base + ".dat", "wb").write(vol.tobytes())
+    H.write_ec_files(base)
+    shas = [_sha(base + H.to_ext(i)) for i in range(14)]
+    # too few shards present -> ErasureCoding(TooFewShardsPresent)
+    for i in range(5):
+        os.rename(base + H.to_ext(i), base + H.to_ext(i) + ".bak")
+    with pytest.raises(H.ErasureCoding) as ei:
+        H.rebuild_ec_files(base)
+    assert isinstance(ei.value.inner, H.TooFewShardsPresent)
+    for i in range(5):
+        os.replace(base + H.to_ext(i) + ".bak", base + H.to_ext(i))
+    # shard 0 one row + 5 bytes long: the second row reads n = 5 != 1 MiB ->
+    # UnexpectedEcShardSize after the first row was rebuilt (encoder.rs:275-280)
+    os.remove(base + H.to_ext(3))
+    with open(base + H.to_ext(0), "r+b") as f:
+        f.truncate((1 << 20) + 5)
+    with pytest.raises(H.UnexpectedEcShardSize):
+        H.rebuild_ec_files(base)
+    assert _sha(base + H.to_ext(3)) == shas[3]
+
+
+def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path):
+    """Shard files smaller than 1 MiB (row = file size), mirrored by the oracle."""
+    import helyim_amd as H
+    rs = O.ReedSolomon(10, 4)
+    L = 1000
+    data = [O.splitmix64_bytes(40 + i, L) for i in range(10)]
+    sh = data + [np.zeros(L, np.uint8) for _ in range(4)]
+    rs.encode(sh)
+    base = str(tmp_path / "w")
+    for i in range(14):
+        open(base + H.to_ext(i), "wb").write(sh[i].tobytes())
+    for i in (2, 11):
+        os.remove(base + H.to_ext(i))
+    assert H.rebuild_ec_files(base) == [2, 11]
+    for i in range(14):
+        assert open(base + H.to_ext(i), "rb").read() == sh[i].tobytes()

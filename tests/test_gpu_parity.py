@@ -1,0 +1,229 @@
+"""Parity of the HIP path against the oracle (GPU). Every comparison is
+bit-exact: this is GF(2^8) byte arithmetic."""
+import itertools
+
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle import rs_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(rng, L):
+    return rng.integers(0, 256, L, dtype=np.uint8)
+
+
+def test_encode_host_api_golden(gpu, golden):
+    import helyim_amd as H
+    g = golden("encode_vectors.json")
+    rs = H.ReedSolomon(10, 4)
+    for L, ent in g["vectors"].items():
+        L = int(L)
+        data = corc.splitmix64_bytes(g["seed"], 10 * L).reshape(10, L)
+        shards = [data[i].copy() for i in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+        rs.encode(shards)
+        assert [O.sha256(s) for s in shards[10:]] == ent["parity_sha256"], L
+        assert rs.verify(shards)
+        shards[12][L // 2] ^= 1
+        assert not rs.verify(shards)
+
+
+def test_rs_5_5_kat_through_product(gpu, golden):
+    import helyim_amd as H
+    kat = golden("upstream_kat.json")["rs_5_5_one_encode"]
+    shards = [np.array(d, np.uint8) for d in kat["data"]] + [np.zeros(2, np.uint8) for _ in range(5)]
+    H.ReedSolomon(5, 5).encode(shards)
+    assert [s.tolist() for s in shards[5:]] == kat["parity"]
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (3, 2), (17, 3), (4, 6), (1, 1), (12, 9), (30, 2)])
+def test_generic_geometry_encode_reconstruct(gpu, k, m):
+    import helyim_amd as H
+    rng = np.random.default_rng(1000 * k + m)
+    rs, ors = H.ReedSolomon(k, m), O.ReedSolomon(k, m)
+    for L in (1, 17, 1000, 4096 + 3):
+        data = [_rand(rng, L) for _ in range(k)]
+        sh = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+        ref = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+        rs.encode(sh)
+        ors.encode(ref)
+        for a, b in zip(sh, ref):
+            assert np.array_equal(a, b)
+        for _ in range(4):
+            e = int(rng.integers(1, m + 1))
+            erased = set(rng.choice(k + m, e, replace=False).tolist())
+            got = [None if i in erased else ref[i].copy() for i in range(k + m)]
+            rs.reconstruct(got)
+            for i in range(k + m):
+                assert np.array_equal(got[i], ref[i]), (k, m, L, sorted(erased), i)
+
+
+def test_reconstruct_host_api_patterns(gpu):
+    import helyim_amd as H
+    rng = np.random.default_rng(7)
+    rs = H.ReedSolomon(10, 4)
+    L = 65536 + 7
+    full = [_rand(rng, L) for _ in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+    O.ReedSolomon(10, 4).encode(full)
+    pats = [c for e in range(1, 5) for c in itertools.combinations(range(14), e)]
+    for idx in rng.choice(len(pats), 60, replace=False):
+        erased = set(pats[idx])
+        got = [None if i in erased else full[i].copy() for i in range(14)]
+        rs.reconstruct(got)
+        for i in range(14):
+            assert np.array_equal(got[i], full[i])
+        got = [None if i in erased else full[i].copy() for i in range(14)]
+        rs.reconstruct_data(got)
+        for i in range(14):
+            if i in erased and i >= 10:
+                assert got[i] is None
+            else:
+                assert np.array_equal(got[i], full[i])
+    with pytest.raises(H.TooFewShardsPresent):
+        rs.reconstruct([None] * 5 + full[5:])
+
+
+def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):
+    import torch
+    import helyim_amd.batch as B
+    t = torch.empty((S, 14, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t, 10 * L, seed_base)
+    return t
+
+
+def test_fill_splitmix_matches_oracle(gpu):
+    S, L = 3, 4097
+    t = _stripes(S, L).cpu().numpy()
+    for s in range(S):
+        ref = corc.splitmix64_bytes(O.STRIPE_SEED_BASE + s, 10 * L).reshape(10, L)
+        assert np.array_equal(t[s, :10], ref)
+
+
+@pytest.mark.parametrize("L", [1, 15, 16, 17, 255, 4096, 4097, 8192 + 16, 65536, 1 << 20])
+def test_batch_encode_vs_oracle(gpu, L):
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    S = 6
+    rs = H.ReedSolomon(10, 4)
+    t = _stripes(S, L)
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    ref = corc.encode_stripes(np.ascontiguousarray(host[:, :10]))
+    assert np.array_equal(host[:, 10:], ref)
+
+
+@pytest.mark.parametrize("vec", [1, 2, 4])
+@pytest.mark.parametrize("max_blocks", [0, 97])
+def test_launch_configs_identical(gpu, vec, max_blocks):
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = 9, 3 * 8192 + 48
+    t = _stripes(S, L)
+    ref = t.clone()
+    B.set_launch_config(2, 0)
+    B.encode_batch(rs, ref)
+    try:
+        B.set_launch_config(vec, max_blocks)
+        B.encode_batch(rs, t)
+    finally:
+        B.set_launch_config(2, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+
+
+def test_batch_encode_separate_and_unaligned(gpu):
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = 4, 5000
+    raw = torch.randint(0, 256, (S * 10 * L + 3,), dtype=torch.uint8, device="cuda")
+    data = raw[3:].view(S, 10, L)  # 3-byte offset: unaligned path
+    par = torch.zeros((S, 4, L), dtype=torch.uint8, device="cuda")
+    B.encode_batch_sep(rs, data, par)
+    torch.cuda.synchronize()
+    ref = corc.encode_stripes(data.cpu().numpy().copy())
+    assert np.array_equal(par.cpu().numpy(), ref)
+
+
+def test_batch_reconstruct_every_pattern(gpu):
+    """All 1470 erasure patterns with 1..4 erasures, one per stripe, one launch."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    pats = [c for e in range(1, 5) for c in itertools.combinations(range(14), e)]
+    assert len(pats) == 1470
+    S, L = len(pats) + 1, 1024 + 48 + 5
+    t = _stripes(S, L)
+    B.encode_batch(rs, t)
+    good = t.clone()
+    masks = np.full(S, (1 << 14) - 1, dtype=np.int32)  # last stripe: nothing erased
+    for s, p in enumerate(pats):
+        for i in p:
+            t[s, i] = 0xA5
+            masks[s] &= ~(1 << i)
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda(), bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0
+    assert torch.equal(t, good)
+
+
+def test_batch_reconstruct_too_few_present(gpu):
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = 3, 4096
+    t = _stripes(S, L)
+    B.encode_batch(rs, t)
+    before = t.clone()
+    masks = torch.tensor([(1 << 14) - 1 - 1, (1 << 14) - 1 - 0b11111, (1 << 14) - 1], dtype=torch.int32,
+                         device="cuda")
+    t[0, 0] = 0
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.reconstruct_batch(rs, t, masks, bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 1
+    assert torch.equal(t[1], before[1])          # skipped, untouched
+    assert torch.equal(t[0], before[0])           # shard 0 rebuilt
+    ref = corc.encode_stripes(before[0:1, :10].cpu().numpy().copy())
+    assert np.array_equal(t[0, 10:].cpu().numpy(), ref[0])
+
+
+def test_full_config_roundtrip(gpu):
+    """BASELINE config 2/3 sizes (4096 x 1 MiB): encode -> erase 4 random shards
+    per stripe -> reconstruct == original; sampled stripes vs the C oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = 4096, 1 << 20
+    t = _stripes(S, L)
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(3)
+    for s in (0, 1, 2047, 4095):
+        ref = corc.encode_stripes(t[s:s + 1, :10].cpu().numpy().copy())
+        assert np.array_equal(t[s, 10:].cpu().numpy(), ref[0])
+    parity_sum = t[:, 10:].view(torch.int64).sum(dtype=torch.int64).item()
+    masks = np.zeros(S, dtype=np.int32)
+    erased = np.zeros((S, 14), dtype=bool)
+    for s in range(S):
+        e = rng.choice(14, 4, replace=False)
+        erased[s, e] = True
+        masks[s] = ((1 << 14) - 1) & ~int(sum(1 << int(i) for i in e))
+    er = torch.from_numpy(erased).cuda()
+    snap = t[er].clone()  # [S*4, L]
+    t[er] = 0
+    B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(t[er], snap)
+    assert t[:, 10:].view(torch.int64).sum(dtype=torch.int64).item() == parity_sum

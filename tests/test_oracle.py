@@ -1,0 +1,207 @@
+"""The oracle itself: pinned to the upstream KATs and the committed fixtures,
+and the numpy and C restatements cross-checked against each other (CPU)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle import rs_oracle as O
+
+
+def test_gf_kats(golden):
+    kat = golden("upstream_kat.json")
+    for a, b, out in kat["gf_mul"]:
+        assert O.gf_mul(a, b) == out
+        assert corc.lib().orc_gf_mul(a, b) == out
+    for a, b, out in kat["gf_div"]:
+        assert O.gf_div(a, b) == out
+    for a, n, out in kat["gf_exp"]:
+        assert O.gf_exp(a, n) == out
+        assert corc.lib().orc_gf_exp(a, n) == out
+
+
+def test_matrix_kats(golden):
+    kat = golden("upstream_kat.json")
+    mm = kat["matrix_mul"]
+    out = O.mat_mul(np.array(mm["a"], np.uint8), np.array(mm["b"], np.uint8))
+    assert out.tolist() == mm["out"]
+    for case in kat["matrix_inverse"]:
+        m = np.array(case["m"], np.uint8)
+        assert O.mat_invert(m).tolist() == case["inv"]
+        cinv = np.zeros_like(m)
+        assert corc.lib().orc_invert(m.ctypes.data, cinv.ctypes.data, m.shape[0]) == 0
+        assert cinv.tolist() == case["inv"]
+
+
+def test_singular_matrix():
+    m = np.array([[1, 2], [2, 4]], np.uint8)
+    with pytest.raises(O.SingularMatrix):
+        O.mat_invert(m)
+
+
+def test_rs_5_5_one_encode(golden):
+    kat = golden("upstream_kat.json")["rs_5_5_one_encode"]
+    for impl in ("py", "c"):
+        shards = [np.array(d, np.uint8) for d in kat["data"]] + [np.zeros(2, np.uint8) for _ in range(5)]
+        if impl == "py":
+            O.ReedSolomon(5, 5).encode(shards)
+        else:
+            corc.CReedSolomon(5, 5).encode(shards, simd=False)
+        assert [s.tolist() for s in shards[5:]] == kat["parity"]
+
+
+def test_rs_10_4_matrix(golden):
+    kat = golden("upstream_kat.json")
+    rs = O.ReedSolomon(10, 4)
+    assert np.array_equal(rs.matrix[:10], np.eye(10, dtype=np.uint8))
+    assert rs.parity_rows.tolist() == kat["rs_10_4_parity_rows"]
+    assert corc.CReedSolomon(10, 4).matrix().tolist() == rs.matrix.tolist()
+    assert golden("tables.json")["matrix_10_4"] == rs.matrix.tolist()
+
+
+def test_tables_fixture(golden):
+    t = golden("tables.json")
+    assert O.sha256(O.EXP_TABLE[:255]) == t["exp_sha256"]
+    assert O.sha256(O.LOG_TABLE[1:].astype(np.uint8)) == t["log_sha256"]
+    assert O.sha256(O.MUL_TABLE) == t["mul_sha256"]
+
+
+def test_splitmix_py_vs_c():
+    for seed, n in [(0x5EED0000, 1), (0x5EED0000, 13), (0x5EED0007, 4096 + 5), (123, 100000)]:
+        assert np.array_equal(O.splitmix64_bytes(seed, n), corc.splitmix64_bytes(seed, n))
+
+
+def test_encode_vectors_fixture(golden):
+    g = golden("encode_vectors.json")
+    rs = O.ReedSolomon(10, 4)
+    for L, ent in g["vectors"].items():
+        L = int(L)
+        if L > 65536:
+            continue  # 1 MiB case is covered by the C oracle below
+        data = O.stripe_data(0, L)
+        assert O.sha256(data) == ent["data_sha256"]
+        shards = [data[i].copy() for i in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+        rs.encode(shards)
+        assert [O.sha256(s) for s in shards[10:]] == ent["parity_sha256"]
+        if "parity_hex" in ent:
+            assert [s.tobytes().hex() for s in shards[10:]] == ent["parity_hex"]
+
+
+@pytest.mark.parametrize("simd", [False, True])
+def test_c_oracle_encode_vectors(golden, simd):
+    g = golden("encode_vectors.json")
+    crs = corc.CReedSolomon(10, 4)
+    for L, ent in g["vectors"].items():
+        L = int(L)
+        data = corc.splitmix64_bytes(g["seed"], 10 * L).reshape(10, L)
+        shards = [data[i].copy() for i in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+        crs.encode(shards, simd=simd)
+        assert [O.sha256(s) for s in shards[10:]] == ent["parity_sha256"], L
+
+
+def test_decode_matrices_fixture(golden):
+    rs = O.ReedSolomon(10, 4)
+    for key, ent in golden("decode_matrices.json").items():
+        pat = [int(x) for x in key.split(",")]
+        present = [i for i in range(14) if i not in pat]
+        assert present[:10] == ent["valid"]
+        assert O.mat_invert(rs.matrix[ent["valid"], :]).tolist() == ent["inverse"]
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (3, 2), (17, 3), (4, 6), (1, 1)])
+def test_reconstruct_py_vs_c(k, m):
+    rng = np.random.default_rng(k * 100 + m)
+    L = 257
+    rs, crs = O.ReedSolomon(k, m), corc.CReedSolomon(k, m)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    full = data + [np.zeros(L, np.uint8) for _ in range(m)]
+    rs.encode(full)
+    cfull = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+    crs.encode(cfull)
+    for a, b in zip(full, cfull):
+        assert np.array_equal(a, b)
+    n = k + m
+    for _ in range(20):
+        e = int(rng.integers(1, m + 1))
+        erased = sorted(rng.choice(n, e, replace=False).tolist())
+        sh = [None if i in erased else full[i].copy() for i in range(n)]
+        rs.reconstruct(sh)
+        csh = [np.zeros(L, np.uint8) if i in erased else full[i].copy() for i in range(n)]
+        assert crs.reconstruct(csh, [i not in erased for i in range(n)]) == 0
+        for i in range(n):
+            assert np.array_equal(sh[i], full[i])
+            assert np.array_equal(csh[i], full[i])
+
+
+def test_reconstruct_errors_and_data_only():
+    rs = O.ReedSolomon(10, 4)
+    L = 33
+    full = [np.full(L, i, np.uint8) for i in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+    rs.encode(full)
+    with pytest.raises(O.TooFewShardsPresent):
+        rs.reconstruct([None] * 5 + full[5:])
+    with pytest.raises(O.TooFewShards):
+        rs.reconstruct(full[:13])
+    with pytest.raises(O.IncorrectShardSize):
+        rs.reconstruct([np.zeros(3, np.uint8)] + full[1:])
+    sh = [None, full[1]] + full[2:12] + [None, None]
+    rs.reconstruct_data(sh)
+    assert np.array_equal(sh[0], full[0]) and sh[12] is None and sh[13] is None
+    with pytest.raises(O.TooFewDataShards):
+        O.ReedSolomon(0, 4)
+    with pytest.raises(O.TooFewParityShards):
+        O.ReedSolomon(4, 0)
+    with pytest.raises(O.TooManyShards):
+        O.ReedSolomon(200, 57)
+
+
+def _manual_layout(dat: bytes, large: int, small: int):
+    """Independent statement of the encoder.rs:200-242 row layout for data shards."""
+    rows = []
+    remaining, pos = len(dat), 0
+    while remaining > large * 10:
+        rows.append((pos, large))
+        pos += large * 10
+        remaining -= large * 10
+    while remaining > 0:
+        rows.append((pos, small))
+        pos += small * 10
+        remaining -= small * 10
+    shards = [b"" for _ in range(10)]
+    for start, block in rows:
+        for i in range(10):
+            chunk = dat[start + i * block: start + (i + 1) * block]
+            shards[i] += chunk + b"\0" * (block - len(chunk))
+    return shards
+
+
+@pytest.mark.parametrize("size", [1, 639, 640, 641, 2000, 6401, 6400 * 2 + 3])
+def test_oracle_file_layout(tmp_path, size):
+    buf, large, small = 16, 640, 32
+    dat = O.splitmix64_bytes(99, size).tobytes()
+    base = str(tmp_path / "v")
+    open(base + ".dat", "wb").write(dat)
+    O.write_ec_files(base, buf, large, small)
+    expect = _manual_layout(dat, large, small)
+    rs = O.ReedSolomon(10, 4)
+    got = [open(base + O.to_ext(i), "rb").read() for i in range(14)]
+    for i in range(10):
+        assert got[i] == expect[i]
+    L = len(got[0])
+    shards = [np.frombuffer(g, np.uint8).copy() for g in got]
+    assert rs.verify(shards) and all(len(g) == L for g in got)
+
+
+def test_oracle_block_size_error(tmp_path):
+    base = str(tmp_path / "v")
+    open(base + ".dat", "wb").write(b"x" * 100)
+    with pytest.raises(O.UnexpectedBlockSize):
+        O.write_ec_files(base, 24, 640, 32)
+
+
+def test_volume_fixture(golden, tmp_path):
+    g = golden("volume_30mb.json")
+    vol = O.synthetic_volume(g["dat_bytes"])
+    assert O.sha256(vol) == g["dat_sha256"]
+    assert g["shard_bytes"] == [3 * (1 << 20)] * 14

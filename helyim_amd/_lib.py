@@ -18,6 +18,15 @@ if not os.path.exists(LIB_PATH):
         "or __graft_entry__.build()). helyim_amd has no CPU fallback."
     )
 
+# One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so
+# (SONAME libamdhip64.so.7). Load it first so libhec's DT_NEEDED binds to the
+# same runtime torch uses; device pointers and hipStream_t handles from torch
+# are then valid in libhec. Without torch, the system ROCm runtime is used.
+try:  # pragma: no cover - depends on the environment
+    import torch  # noqa: F401
+except ImportError:
+    torch = None
+
 lib = ctypes.CDLL(LIB_PATH)
 
 _P = ctypes.c_void_p
@@ -47,6 +56,7 @@ SIGNATURES = {
     "hec_write_ec_files_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64]),
     "hec_rebuild_ec_files": (_I, [ctypes.c_char_p, ctypes.POINTER(_U32), ctypes.POINTER(_S)]),
     "hec_set_launch_config": (_I, [_I, ctypes.c_long]),
+    "hec_set_kernel_mode": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
 }
 

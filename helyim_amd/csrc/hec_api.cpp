@@ -409,6 +409,12 @@ int hec_set_launch_config(int vec_per_thread, long max_blocks) {
     return HEC_OK;
 }
 
+int hec_set_kernel_mode(int mode) {
+    if (mode != 0 && mode != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "mode must be 0 or 1");
+    launch_config().mode = mode;
+    return HEC_OK;
+}
+
 int hec_rs_new(size_t data_shards, size_t parity_shards, hec_rs_t** out) {
     if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
     *out = nullptr;

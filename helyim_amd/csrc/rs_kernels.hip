@@ -88,11 +88,23 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R], const u32x4 d, const __a
 
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
+// Diagnostic bandwidth ceiling: same loads/stores/addressing, GF math replaced
+// by a plain XOR (wrong parity by design; never used by the product paths).
+template <int R, bool XORONLY>
+__device__ __forceinline__ void mac(u32x4 (&acc)[R], const u32x4 d, cu32p tab) {
+    if constexpr (XORONLY) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] ^= d;
+    } else {
+        gf_mac<R>(acc, d, tab);
+    }
+}
+
 // One group of R (<= 4) output rows of a plan over U vectors per lane.
 // K > 0: compile-time input count (all K loads issued before any math);
 // K == 0: runtime nin loop. Lanes whose 16-byte vector crosses the end of the
 // shard take the byte-wise tail path (only in the last chunk of a stripe).
-template <int K, int R, int U, bool ALIGNED>
+template <int K, int R, int U, bool ALIGNED, bool XORONLY = false>
 __device__ __forceinline__ void apply_group(const ApplyArgs& a, const uint8_t* in_b, uint8_t* out_b,
                                             cu32p in_ids, cu32p out_ids, cu32p tab, uint32_t nin,
                                             uint32_t tab_row_stride, uint64_t chunk_off) {
@@ -111,7 +123,7 @@ __device__ __forceinline__ void apply_group(const ApplyArgs& a, const uint8_t* i
                 for (int i = 0; i < K; ++i)
                     d[i] = load_full(in_b + uint64_t(in_ids[i]) * a.in_shard + o, ALIGNED);
 #pragma unroll
-                for (int i = 0; i < K; ++i) gf_mac<R>(acc, d[i], tab + i * tab_row_stride);
+                for (int i = 0; i < K; ++i) mac<R, XORONLY>(acc, d[i], tab + i * tab_row_stride);
             } else {
                 for (uint32_t i = 0; i < nin; ++i) {
                     const u32x4 d = load_full(in_b + uint64_t(in_ids[i]) * a.in_shard + o, ALIGNED);
@@ -132,7 +144,7 @@ __device__ __forceinline__ void apply_group(const ApplyArgs& a, const uint8_t* i
     }
 }
 
-template <int K, int U, bool ALIGNED>
+template <int K, int U, bool ALIGNED, bool XORONLY = false>
 __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
     for (uint64_t item = blockIdx.x; item < a.n_items; item += gridDim.x) {
         const uint32_t stripe = uint32_t(item / a.chunks_per_stripe);
@@ -159,16 +171,16 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
             const uint32_t R = p.nout - g < 4 ? p.nout - g : 4;
             cu32p tg = tab + g * 5;
             switch (R) {
-                case 4: apply_group<K, 4, U, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
-                case 3: apply_group<K, 3, U, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
-                case 2: apply_group<K, 2, U, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
-                default: apply_group<K, 1, U, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                case 4: apply_group<K, 4, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                case 3: apply_group<K, 3, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                case 2: apply_group<K, 2, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                default: apply_group<K, 1, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
             }
         }
     }
 }
 
-template <int K, int U, bool ALIGNED>
+template <int K, int U, bool ALIGNED, bool XORONLY = false>
 static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
     const uint64_t chunk = uint64_t(U) * kThreads * kVecBytes;
     a.chunks_per_stripe = uint32_t((a.len + chunk - 1) / chunk);
@@ -177,12 +189,19 @@ static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t str
     uint64_t grid = a.n_items;
     if (cfg.max_blocks > 0 && grid > uint64_t(cfg.max_blocks)) grid = uint64_t(cfg.max_blocks);
     if (grid > 0x7FFFFFFFull) grid = 0x7FFFFFFFull;
-    hipLaunchKernelGGL((rs_apply_kernel<K, U, ALIGNED>), dim3(uint32_t(grid)), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL((rs_apply_kernel<K, U, ALIGNED, XORONLY>), dim3(uint32_t(grid)), dim3(kThreads), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
                         hipStream_t stream) {
+    if (nin == 10 && aligned && cfg.mode == 1) {
+        switch (cfg.vec_per_thread) {
+            case 1: return launch_t<10, 1, true, true>(a, cfg, stream);
+            case 4: return launch_t<10, 4, true, true>(a, cfg, stream);
+            default: return launch_t<10, 2, true, true>(a, cfg, stream);
+        }
+    }
     if (nin == 10 && aligned) {
         switch (cfg.vec_per_thread) {
             case 1: return launch_t<10, 1, true>(a, cfg, stream);

@@ -161,6 +161,11 @@ int hec_rebuild_ec_files(const char* base_filename, uint32_t* rebuilt_ids, size_
 /* Kernel launch configuration: 16-byte vectors per lane per chunk (1, 2, 4)
  * and grid cap (0 = one workgroup per chunk). Returns previous values. */
 int hec_set_launch_config(int vec_per_thread, long max_blocks);
+/* Diagnostic: 0 = GF(2^8) coding (default); 1 = XOR-only bandwidth ceiling --
+ * the RS(10,4) aligned kernel with its GF math replaced by plain XOR (same
+ * loads, stores and addressing; WRONG parity by design), used only to measure
+ * the achievable HBM rate of this access pattern. Returns HEC_OK. */
+int hec_set_kernel_mode(int mode);
 /* Version string of the library build. */
 const char* hec_version(void);
 

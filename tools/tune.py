@@ -1,0 +1,74 @@
+"""Launch-configuration sweep for the RS(10,4) kernels on the BASELINE config
+(4096 x 1 MiB stripes, device-resident). Interleaved rounds in one process
+(cdna_hip_programming.md §5.4 rule 24); prints one JSON line per config with
+the median/min encode and decode ms and HBM GB/s, plus the XOR-only ceiling.
+
+python tools/tune.py [--stripes 4096] [--rounds 5]
+"""
+import argparse
+import itertools
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--shard-len", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--vecs", default="1,2,4")
+    ap.add_argument("--blocks", default="0,2048,4096,8192")
+    args = ap.parse_args()
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    import bench
+    S, L = args.stripes, args.shard_len
+    rs = H.ReedSolomon(10, 4)
+    t = torch.empty((S, 14, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t, 10 * L, 0x5EED0000)
+    masks = torch.from_numpy(bench.erasure_masks(S, 0)).cuda()
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    good = t[:8].clone()
+    configs = [(mode, v, b) for mode in (0, 1)
+               for v, b in itertools.product([int(x) for x in args.vecs.split(",")],
+                                             [int(x) for x in args.blocks.split(",")])]
+    res = {c: {"enc": [], "dec": []} for c in configs}
+    s = torch.cuda.current_stream()
+    for _ in range(args.rounds):
+        for c in configs:
+            mode, v, b = c
+            H.lib.hec_set_kernel_mode(mode)
+            B.set_launch_config(v, b)
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(s)
+            B.encode_batch(rs, t)
+            e1.record(s)
+            B.reconstruct_batch(rs, t, masks)
+            e2.record(s)
+            torch.cuda.synchronize()
+            res[c]["enc"].append(e0.elapsed_time(e1))
+            res[c]["dec"].append(e1.elapsed_time(e2))
+    H.lib.hec_set_kernel_mode(0)
+    B.set_launch_config(2, 0)
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    assert torch.equal(t[:8], good)
+    nbytes = S * 14 * L
+    for c in configs:
+        enc, dec = np.array(res[c]["enc"]), np.array(res[c]["dec"])
+        print(json.dumps({"mode": ["gf", "xor_ceiling"][c[0]], "vec_per_thread": c[1], "max_blocks": c[2],
+                          "enc_ms_med": round(float(np.median(enc)), 3), "enc_ms_min": round(float(enc.min()), 3),
+                          "enc_GBps": round(nbytes / np.median(enc) / 1e6, 1),
+                          "dec_ms_med": round(float(np.median(dec)), 3),
+                          "dec_GBps": round(nbytes / np.median(dec) / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

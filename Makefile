@@ -23,8 +23,20 @@ build/obj/%.cpp.o: helyim_amd/csrc/%.cpp $(HDR)
 oracle:
 	$(MAKE) -C oracle
 
+# Measurement variants of the kernel file (cache policy of shard streams).
+VARIANTS := ntl0_nts0 ntl0_nts1 ntl1_nts0
+variants: $(foreach v,$(VARIANTS),build/variants/libhec_$(v).so)
+build/variants/libhec_%.so: $(SRC) $(HDR)
+	@mkdir -p build/variants/$*
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c helyim_amd/csrc/rs_kernels.hip -o build/variants/$*/rs_kernels.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ build/variants/$*/rs_kernels.o \
+	    $(filter-out build/obj/rs_kernels.hip.o,$(OBJ)) -lpthread
+VFLAGS_ntl0_nts0 := -DHEC_NT_LOAD=0 -DHEC_NT_STORE=0
+VFLAGS_ntl0_nts1 := -DHEC_NT_LOAD=0 -DHEC_NT_STORE=1
+VFLAGS_ntl1_nts0 := -DHEC_NT_LOAD=1 -DHEC_NT_STORE=0
+
 clean:
 	rm -rf build helyim_amd/libhec.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean variants

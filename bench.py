@@ -128,6 +128,87 @@ def load_traffic() -> dict:
     return {}
 
 
+def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) -> dict:
+    """End-to-end rate from pinned host memory (the path helyim runs): host
+    stripes -> H2D -> kernel -> D2H, pipelined over 3 streams. Encode moves
+    10 L H2D + 4 L D2H per stripe; a 4-erasure decode 10 L H2D + 4 L D2H."""
+    import torch
+    import helyim_amd.batch as B
+    dev = torch.empty((S, N_TOTAL, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(dev, K_DATA * L, rank_seed_base(rank))
+    host = torch.empty((S, N_TOTAL, L), dtype=torch.uint8).pin_memory()
+    host.copy_(dev)
+    del dev
+    masks = erasure_masks(S, rank)
+    B.host_encode_batch(rs, host)  # warm-up (pipeline buffers, tables)
+    B.host_reconstruct_batch(rs, host, masks)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        B.host_encode_batch(rs, host)
+    te = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        B.host_reconstruct_batch(rs, host, masks)
+    td = (time.perf_counter() - t0) / reps
+    data = S * K_DATA * L
+    return {"stripes": S, "shard_len": L, "host_memory": "pinned (torch pin_memory)",
+            "encode_data_GiB_s": round(data / te / 2**30, 2),
+            "decode_data_GiB_s": round(data / td / 2**30, 2),
+            "encode_pcie_GB_s": round(S * N_TOTAL * L / te / 1e9, 2),
+            "decode_pcie_GB_s": round(S * N_TOTAL * L / td / 1e9, 2)}
+
+
+def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
+    """BASELINE config 5: shard lengths 64 KiB..4 MiB (log-uniform), 0..4
+    erasures per stripe; device-resident and end-to-end (pinned host) rates."""
+    import torch
+    import helyim_amd.batch as B
+    rng = np.random.default_rng(0x5E + rank)
+    lens = [(64 << 10) << i for i in range(7)]
+    Ls = rng.choice(lens, n_stripes)
+    es = rng.integers(0, 5, n_stripes)
+    groups = []
+    for L in lens:
+        idx = np.nonzero(Ls == L)[0]
+        if len(idx) == 0:
+            continue
+        full = (1 << N_TOTAL) - 1
+        masks = np.empty(len(idx), dtype=np.int32)
+        for j, s in enumerate(idx):
+            drop = rng.choice(N_TOTAL, int(es[s]), replace=False)
+            masks[j] = full & ~int(sum(1 << int(i) for i in drop))
+        dev = torch.empty((len(idx), N_TOTAL, int(L)), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(dev, K_DATA * int(L), rank_seed_base(rank) + int(L))
+        groups.append((int(L), dev, torch.from_numpy(masks).cuda(), masks))
+    data = sum(g[1].shape[0] * K_DATA * g[0] for g in groups)
+    for _, dev, dm, _ in groups:  # warm-up
+        B.encode_batch(rs, dev)
+        B.reconstruct_batch(rs, dev, dm)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _, dev, dm, _ in groups:
+        B.encode_batch(rs, dev)
+        B.reconstruct_batch(rs, dev, dm)
+    e1.record(s)
+    torch.cuda.synchronize()
+    t_dev = e0.elapsed_time(e1) * 1e-3
+    hosts = [(g[1].cpu().pin_memory(), g[3]) for g in groups]
+    del groups
+    for h, m in hosts:
+        B.host_encode_batch(rs, h)
+    t0 = time.perf_counter()
+    for h, m in hosts:
+        B.host_encode_batch(rs, h)
+        B.host_reconstruct_batch(rs, h, m.astype(np.uint32))
+    t_e2e = time.perf_counter() - t0
+    return {"stripes": n_stripes, "shard_lens": "64 KiB..4 MiB log-uniform", "erasures": "0..4 uniform",
+            "payload_GiB": round(data / 2**30, 3),
+            "device_resident_data_GiB_s": round(2 * data / t_dev / 2**30, 2),
+            "end_to_end_data_GiB_s": round(2 * data / t_e2e / 2**30, 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,6 +218,7 @@ def main():
     ap.add_argument("--shard-len", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the end-to-end and mixed-workload sections")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +326,9 @@ def main():
                        "frac": round(dec_gbps / HBM_PEAK_GBPS, 4)},
             "verified": chk_ok,
         }
+        if world == 1 and not args.no_extras:
+            out["end_to_end"] = e2e_section(rs, rank)
+            out["mixed"] = mixed_section(rs, rank)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhec.so")
+# HEC_LIB_PATH: measurement builds only (tools/tune.py loads kernel variants).
+LIB_PATH = os.environ.get("HEC_LIB_PATH") or os.path.join(_HERE, "libhec.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -51,6 +52,8 @@ SIGNATURES = {
     "hec_rs_reconstruct_data": (_I, [_P, _P, _P, _P, _S]),
     "hec_gpu_encode_batch": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32, _P]),
     "hec_gpu_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P]),
+    "hec_host_encode_batch": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32]),
+    "hec_host_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P]),
     "hec_gpu_fill_splitmix": (_I, [_P, _U64, _U64, _U32, _U64, _P]),
     "hec_write_ec_files": (_I, [ctypes.c_char_p]),
     "hec_write_ec_files_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64]),

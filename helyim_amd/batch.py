@@ -61,6 +61,37 @@ def reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks: tor
                                         _stream_ptr(stream)))
 
 
+def _check_host(t: torch.Tensor):
+    if t.dtype != torch.uint8 or t.is_cuda or t.dim() != 3 or t.stride(2) != 1:
+        raise TypeError("expected a host uint8 tensor [stripes, shards, L] with contiguous shards")
+
+
+def host_encode_batch(rs: ReedSolomon, stripes: torch.Tensor) -> None:
+    """Host-memory stripes[S, total, L] (pin_memory() for full PCIe rate):
+    parity computed on the GPU, pipelined H2D -> kernel -> D2H."""
+    _check_host(stripes)
+    k = rs.data_shard_count()
+    S, n, L = stripes.shape
+    st, sh = stripes.stride(0), stripes.stride(1)
+    base = stripes.data_ptr()
+    check(lib.hec_host_encode_batch(rs.handle, base, st, sh, base + k * sh, st, sh, L, S))
+
+
+def host_reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks) -> int:
+    """Host-memory in-place reconstruct; returns the number of skipped stripes
+    (fewer than data_shards present)."""
+    import ctypes
+    import numpy as np
+    _check_host(stripes)
+    S, n, L = stripes.shape
+    m = np.ascontiguousarray(np.asarray(present_masks, dtype=np.uint32))
+    assert m.size == S
+    bad = ctypes.c_uint32(0)
+    check(lib.hec_host_reconstruct_batch(rs.handle, stripes.data_ptr(), stripes.stride(0), stripes.stride(1), L,
+                                         S, m.ctypes.data, ctypes.byref(bad)))
+    return int(bad.value)
+
+
 def fill_splitmix(t: torch.Tensor, bytes_per_stripe: int, seed_base: int, stream=None) -> None:
     """Fill the first bytes_per_stripe bytes of each t[s] with splitmix64(seed_base + s)."""
     S = t.shape[0]
@@ -68,5 +99,5 @@ def fill_splitmix(t: torch.Tensor, bytes_per_stripe: int, seed_base: int, stream
                                     _stream_ptr(stream)))
 
 
-def set_launch_config(vec_per_thread: int = 2, max_blocks: int = 0) -> None:
+def set_launch_config(vec_per_thread: int = 1, max_blocks: int = 0) -> None:
     check(lib.hec_set_launch_config(vec_per_thread, max_blocks))

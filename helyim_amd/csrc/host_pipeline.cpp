@@ -1,0 +1,216 @@
+// Host-memory stripe batches through the GPU: the path helyim actually runs
+// (shard bytes start and end in host memory: .dat pages / shard files,
+// helyim-ec/src/encoder.rs:169-195, 263-304). Chunks of stripes are pipelined
+// over kDepth HIP streams, each with its own device slot, so the H2D copy of
+// chunk i+1, the kernel of chunk i and the D2H copy of chunk i-1 overlap
+// (PCIe Gen5 x16 is full duplex; the copy engines run beside the kernel).
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+
+#include "hec_internal.hpp"
+
+namespace hec {
+namespace {
+
+constexpr int kDepth = 3;
+constexpr uint64_t kChunkBytes = 96ull << 20;  // target bytes of one chunk's 14 shards
+
+struct Pipeline {
+    std::mutex mu;
+    hipStream_t streams[kDepth] = {};
+    uint8_t* slot[kDepth] = {};
+    uint32_t* mask_dev[kDepth] = {};
+    uint32_t* mask_host[kDepth] = {};  // pinned staging for per-chunk masks
+    size_t slot_cap = 0, mask_cap = 0;
+    ~Pipeline() {
+        for (int i = 0; i < kDepth; ++i) {
+            (void)hipFree(slot[i]);
+            (void)hipFree(mask_dev[i]);
+            (void)hipHostFree(mask_host[i]);
+            if (streams[i]) (void)hipStreamDestroy(streams[i]);
+        }
+    }
+    int reserve(size_t slot_bytes, size_t n_masks) {
+        if (!streams[0])
+            for (int i = 0; i < kDepth; ++i) HEC_HIP(hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking));
+        if (slot_bytes > slot_cap) {
+            for (int i = 0; i < kDepth; ++i) {
+                if (slot[i]) HEC_HIP(hipFree(slot[i]));
+                slot[i] = nullptr;
+            }
+            slot_cap = 0;
+            for (int i = 0; i < kDepth; ++i) HEC_HIP(hipMalloc(reinterpret_cast<void**>(&slot[i]), slot_bytes));
+            slot_cap = slot_bytes;
+        }
+        if (n_masks > mask_cap) {
+            for (int i = 0; i < kDepth; ++i) {
+                if (mask_dev[i]) HEC_HIP(hipFree(mask_dev[i]));
+                if (mask_host[i]) HEC_HIP(hipHostFree(mask_host[i]));
+                mask_dev[i] = mask_host[i] = nullptr;
+            }
+            mask_cap = 0;
+            for (int i = 0; i < kDepth; ++i) {
+                HEC_HIP(hipMalloc(reinterpret_cast<void**>(&mask_dev[i]), n_masks * 4));
+                HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&mask_host[i]), n_masks * 4, hipHostMallocDefault));
+            }
+            mask_cap = n_masks;
+        }
+        return HEC_OK;
+    }
+};
+
+std::mutex g_pipe_mu;
+std::map<int, std::unique_ptr<Pipeline>> g_pipes;
+
+int pipeline(Pipeline** out) {
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    auto& p = g_pipes[dev];
+    if (!p) p.reset(new Pipeline());
+    *out = p.get();
+    return HEC_OK;
+}
+
+// Copy `rows` rows of `width` bytes with pitches (2D; 1D when both are dense).
+hipError_t copy2d(void* dst, uint64_t dpitch, const void* src, uint64_t spitch, uint64_t width, uint64_t rows,
+                  hipMemcpyKind kind, hipStream_t s) {
+    if (rows == 0 || width == 0) return hipSuccess;
+    if (rows == 1 || (dpitch == width && spitch == width))
+        return hipMemcpyAsync(dst, src, width * rows, kind, s);
+    return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s);
+}
+
+uint32_t chunk_stripes(uint64_t shard_len, int n, uint32_t n_stripes) {
+    uint64_t c = std::max<uint64_t>(1, kChunkBytes / (uint64_t(n) * shard_len));
+    return uint32_t(std::min<uint64_t>(c, n_stripes));
+}
+
+}  // namespace
+}  // namespace hec
+
+using namespace hec;
+
+extern "C" {
+
+int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t data_stripe_stride,
+                          uint64_t data_shard_stride, uint8_t* h_parity, uint64_t parity_stripe_stride,
+                          uint64_t parity_shard_stride, uint64_t shard_len, uint32_t n_stripes) {
+    if (!rs || !h_data || !h_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (n_stripes == 0) return HEC_OK;
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    Pipeline* p;
+    if ((rc = pipeline(&p))) return rc;
+    std::lock_guard<std::mutex> lk(p->mu);
+    const int k = rs->k, m = rs->m;
+    const uint64_t Lp = (shard_len + 255) / 256 * 256;  // device shard pitch
+    const uint32_t C = chunk_stripes(Lp, rs->n, n_stripes);
+    if ((rc = p->reserve(size_t(C) * rs->n * Lp, 1))) return rc;
+    const uint64_t dstripe = uint64_t(rs->n) * Lp;
+    for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
+        const uint32_t c = std::min(C, n_stripes - s0);
+        const int q = int(it % kDepth);
+        hipStream_t st = p->streams[q];
+        uint8_t* d = p->slot[q];
+        for (uint32_t s = 0; s < c; ++s)  // data shards of stripe s -> [s][0..k)
+            HEC_HIP(copy2d(d + s * dstripe, Lp, h_data + (s0 + s) * data_stripe_stride, data_shard_stride,
+                           shard_len, uint64_t(k), hipMemcpyHostToDevice, st));
+        // len rounded to 16: the pad bytes of the device pitch are computed but never copied back
+        if ((rc = run_apply(gd->encode, uint32_t(k), d, dstripe, Lp, d + uint64_t(k) * Lp, dstripe, Lp,
+                            (shard_len + 15) / 16 * 16, c, nullptr, nullptr, st)))
+            return rc;
+        for (uint32_t s = 0; s < c; ++s)
+            HEC_HIP(copy2d(h_parity + (s0 + s) * parity_stripe_stride, parity_shard_stride,
+                           d + s * dstripe + uint64_t(k) * Lp, Lp, shard_len, uint64_t(m), hipMemcpyDeviceToHost, st));
+    }
+    for (int q = 0; q < kDepth; ++q) HEC_HIP(hipStreamSynchronize(p->streams[q]));
+    return HEC_OK;
+}
+
+int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t stripe_stride, uint64_t shard_stride,
+                               uint64_t shard_len, uint32_t n_stripes, const uint32_t* h_present_masks,
+                               uint32_t* n_bad_stripes) {
+    if (!rs || !h_shards || !h_present_masks) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (n_bad_stripes) *n_bad_stripes = 0;
+    if (n_stripes == 0) return HEC_OK;
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    Pipeline* p;
+    if ((rc = pipeline(&p))) return rc;
+    std::lock_guard<std::mutex> lk(p->mu);
+    const int k = rs->k, n = rs->n;
+    const uint64_t Lp = (shard_len + 255) / 256 * 256;
+    const uint32_t C = chunk_stripes(Lp, n, n_stripes);
+    if ((rc = p->reserve(size_t(C) * n * Lp, C))) return rc;
+    if ((rc = ensure_dense_decode(rs, gd, p->streams[0]))) return rc;
+    const uint64_t dstripe = uint64_t(n) * Lp;
+    const uint32_t full = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
+    uint32_t bad = 0;
+    for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
+        const uint32_t c = std::min(C, n_stripes - s0);
+        const int q = int(it % kDepth);
+        hipStream_t st = p->streams[q];
+        uint8_t* d = p->slot[q];
+        // the staging of this slot was last read by the copy issued kDepth chunks ago
+        HEC_HIP(hipStreamSynchronize(st));
+        for (uint32_t s = 0; s < c; ++s) {
+            const uint32_t mask = h_present_masks[s0 + s] & full;
+            p->mask_host[q][s] = mask;
+            const int present = __builtin_popcount(mask);
+            if (present < k) {
+                ++bad;
+                continue;
+            }
+            if (present == n) continue;
+            // H2D only the first k present shards (the ones the decode reads),
+            // merged into runs of adjacent shard ids.
+            int used = 0;
+            for (int i = 0; i < n && used < k;) {
+                if (!((mask >> i) & 1)) {
+                    ++i;
+                    continue;
+                }
+                int j = i;
+                while (j < n && ((mask >> j) & 1) && used + (j - i) < k) ++j;
+                HEC_HIP(copy2d(d + s * dstripe + uint64_t(i) * Lp, Lp,
+                               h_shards + (s0 + s) * stripe_stride + uint64_t(i) * shard_stride, shard_stride,
+                               shard_len, uint64_t(j - i), hipMemcpyHostToDevice, st));
+                used += j - i;
+                i = j;
+            }
+        }
+        HEC_HIP(hipMemcpyAsync(p->mask_dev[q], p->mask_host[q], c * 4, hipMemcpyHostToDevice, st));
+        if ((rc = run_apply(gd->decode_dense, uint32_t(k), d, dstripe, Lp, d, dstripe, Lp,
+                            (shard_len + 15) / 16 * 16, c, p->mask_dev[q], nullptr, st)))
+            return rc;
+        for (uint32_t s = 0; s < c; ++s) {
+            const uint32_t mask = p->mask_host[q][s];
+            if (__builtin_popcount(mask) < k) continue;
+            for (int i = 0; i < n;) {  // D2H the erased shards, merged into runs
+                if ((mask >> i) & 1) {
+                    ++i;
+                    continue;
+                }
+                int j = i;
+                while (j < n && !((mask >> j) & 1)) ++j;
+                HEC_HIP(copy2d(h_shards + (s0 + s) * stripe_stride + uint64_t(i) * shard_stride, shard_stride,
+                               d + s * dstripe + uint64_t(i) * Lp, Lp, shard_len, uint64_t(j - i),
+                               hipMemcpyDeviceToHost, st));
+                i = j;
+            }
+        }
+    }
+    for (int q = 0; q < kDepth; ++q) HEC_HIP(hipStreamSynchronize(p->streams[q]));
+    if (n_bad_stripes) *n_bad_stripes = bad;
+    return HEC_OK;
+}
+
+}  // extern "C"

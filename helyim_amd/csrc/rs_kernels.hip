@@ -30,8 +30,23 @@ __device__ __forceinline__ const __attribute__((address_space(4))) T* as_const(c
     return (const __attribute__((address_space(4))) T*)(p);
 }
 
+// Cache policy of the streamed shard bytes (each is touched exactly once).
+// Build-time switches for measurement variants (tools/tune.py).
+#ifndef HEC_NT_LOAD
+#define HEC_NT_LOAD 1
+#endif
+#ifndef HEC_NT_STORE
+#define HEC_NT_STORE 1
+#endif
+
 __device__ __forceinline__ u32x4 load_full(const uint8_t* p, bool aligned) {
-    if (aligned) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    if (aligned) {
+#if HEC_NT_LOAD
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+        return *reinterpret_cast<const u32x4*>(p);
+#endif
+    }
     u32x4 v;
     __builtin_memcpy(&v, p, 16);
     return v;
@@ -39,7 +54,11 @@ __device__ __forceinline__ u32x4 load_full(const uint8_t* p, bool aligned) {
 
 __device__ __forceinline__ void store_full(uint8_t* p, u32x4 v, bool aligned) {
     if (aligned) {
+#if HEC_NT_STORE
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+#else
+        *reinterpret_cast<u32x4*>(p) = v;
+#endif
     } else {
         __builtin_memcpy(p, &v, 16);
     }

@@ -41,7 +41,7 @@ struct ApplyArgs {
 };
 
 struct LaunchConfig {
-    int vec_per_thread = 2;      // 16-byte vectors per lane per chunk (1, 2 or 4)
+    int vec_per_thread = 1;      // 16-byte vectors per lane per chunk (1, 2 or 4)
     long max_blocks = 0;         // grid cap (0 = one block per chunk)
     int mode = 0;                // 0 = GF coding; 1 = XOR-only bandwidth ceiling (diagnostic)
 };

@@ -137,6 +137,25 @@ int hec_gpu_reconstruct_batch(const hec_rs_t* rs, uint8_t* d_shards, uint64_t st
                               const uint32_t* d_present_masks, uint32_t* d_bad_stripes,
                               void* stream);
 
+/* ---- host-memory batches (the path helyim runs: bytes start and end in host
+ * memory, encoder.rs:169-195 / 263-304) -------------------------------------
+ * Same strided layout as above but on HOST pointers. Chunks of stripes are
+ * pipelined H2D -> kernel -> D2H over 3 HIP streams so copies overlap the
+ * kernels; synchronous on return. Pin the host buffers (hipHostMalloc,
+ * torch pin_memory) for full PCIe rate; pageable memory works, slower. */
+int hec_host_encode_batch(const hec_rs_t* rs,
+                          const uint8_t* h_data, uint64_t data_stripe_stride, uint64_t data_shard_stride,
+                          uint8_t* h_parity, uint64_t parity_stripe_stride, uint64_t parity_shard_stride,
+                          uint64_t shard_len, uint32_t n_stripes);
+/* Reconstruct in place with per-stripe host masks (bit i = shard i present):
+ * only the first data_shards present shards of a stripe cross PCIe H2D and
+ * only its erased shards cross D2H. Stripes with fewer than data_shards
+ * present are skipped and counted into *n_bad_stripes (optional). Requires
+ * total shards <= 16. */
+int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t stripe_stride,
+                               uint64_t shard_stride, uint64_t shard_len, uint32_t n_stripes,
+                               const uint32_t* h_present_masks, uint32_t* n_bad_stripes);
+
 /* Deterministic splitmix64 stripe data (bench / test inputs): stripe s gets
  * bytes_per_stripe bytes at d_base + s*stripe_stride, 64-bit word n (n >= 1)
  * = splitmix64_mix(seed_base + s + n * 0x9E3779B97F4A7C15), little endian. */

@@ -126,13 +126,13 @@ def test_launch_configs_identical(gpu, vec, max_blocks):
     S, L = 9, 3 * 8192 + 48
     t = _stripes(S, L)
     ref = t.clone()
-    B.set_launch_config(2, 0)
+    B.set_launch_config(1, 0)
     B.encode_batch(rs, ref)
     try:
         B.set_launch_config(vec, max_blocks)
         B.encode_batch(rs, t)
     finally:
-        B.set_launch_config(2, 0)
+        B.set_launch_config(1, 0)
     torch.cuda.synchronize()
     assert torch.equal(t, ref)
 

@@ -1,0 +1,61 @@
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes of bench.py into
+profiles/pmc_traffic.json (HBM bytes per launch of the RS kernels).
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7):
+FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE reports exactly half the
+bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
+WRITE_SIZE is exact for 16 B/lane streaming stores.
+
+bench.py launches encode and decode alternately on the same full-size batch,
+so full-grid dispatches alternate encode (even position) / decode (odd).
+usage: python tools/pmc_summary.py gpurun_out/prof_r01 profiles/pmc_traffic.json
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+
+def load(path, counter):
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    full = max(int(r["Grid_Size"]) for r in rows)
+    rows = [r for r in rows if int(r["Grid_Size"]) == full]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    return [float(r["Counter_Value"]) * 1024 for r in rows], rows[0]["Kernel_Name"], full
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    fetch, kname, grid = load(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write, _, _ = load(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    enc_r = statistics.median(fetch[0::2]) * 2
+    dec_r = statistics.median(fetch[1::2]) * 2
+    enc_w = statistics.median(write[0::2])
+    dec_w = statistics.median(write[1::2])
+    S, L = 4096, 1 << 20
+    out = {
+        "source": src,
+        "kernel": kname,
+        "grid_size_threads": grid,
+        "workload": f"{S} stripes x {L} B, RS(10,4)",
+        "correction": "FETCH_SIZE*1024*2 (gfx950 half-count on 16B/lane streams), WRITE_SIZE*1024",
+        "encode_hbm_read_bytes_per_launch": enc_r,
+        "encode_hbm_write_bytes_per_launch": enc_w,
+        "encode_hbm_bytes_per_launch": enc_r + enc_w,
+        "encode_algorithmic_bytes_per_launch": 14 * S * L,
+        "decode_hbm_read_bytes_per_launch": dec_r,
+        "decode_hbm_write_bytes_per_launch": dec_w,
+        "decode_hbm_bytes_per_launch": dec_r + dec_w,
+        "decode_algorithmic_bytes_per_launch": 14 * S * L,
+    }
+    out["encode_traffic_over_algorithmic"] = out["encode_hbm_bytes_per_launch"] / out["encode_algorithmic_bytes_per_launch"]
+    out["decode_traffic_over_algorithmic"] = out["decode_hbm_bytes_per_launch"] / out["decode_algorithmic_bytes_per_launch"]
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+        f.write("\n")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

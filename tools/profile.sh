@@ -1,0 +1,16 @@
+# rocprofv3 evidence for the bench command (run on the GPU box from the repo root):
+#   1) kernel trace + stats of the default bench (kernel durations)
+#   2) FETCH_SIZE pass, 3) WRITE_SIZE pass -- separate PMC passes (gfx950 TCC slots),
+#      restricted to the RS kernels. Outputs under gpurun_out/$TAG/.
+set -e
+TAG=${1:-prof}
+OUT=gpurun_out/$TAG
+export TMPDIR=/tmp
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras > $OUT/bench_trace.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex rs_apply --output-format csv \
+    -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --kernel-include-regex rs_apply --output-format csv \
+    -d $OUT/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_write.log 2>&1
+find $OUT -name "*.csv" | sort

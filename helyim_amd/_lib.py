@@ -58,7 +58,7 @@ SIGNATURES = {
     "hec_write_ec_files": (_I, [ctypes.c_char_p]),
     "hec_write_ec_files_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64]),
     "hec_rebuild_ec_files": (_I, [ctypes.c_char_p, ctypes.POINTER(_U32), ctypes.POINTER(_S)]),
-    "hec_set_launch_config": (_I, [_I, ctypes.c_long]),
+    "hec_set_launch_config": (_I, [_I, ctypes.c_long, _I, _I]),
     "hec_set_kernel_mode": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
 }

@@ -99,5 +99,7 @@ def fill_splitmix(t: torch.Tensor, bytes_per_stripe: int, seed_base: int, stream
                                     _stream_ptr(stream)))
 
 
-def set_launch_config(vec_per_thread: int = 1, max_blocks: int = 0) -> None:
-    check(lib.hec_set_launch_config(vec_per_thread, max_blocks))
+def set_launch_config(vec_per_thread: int = 1, max_blocks: int = 0, xcd_remap: int = 1,
+                      blocks_per_cu: int = 0) -> None:
+    """Process-wide kernel launch configuration (speed only; bytes identical)."""
+    check(lib.hec_set_launch_config(vec_per_thread, max_blocks, xcd_remap, blocks_per_cu))

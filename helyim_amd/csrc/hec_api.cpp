@@ -50,15 +50,16 @@ int current_device(int* dev) {
 // ---------------------------------------------------------------------------
 uint32_t HostPlans::add(const Mat& coefs, const std::vector<uint32_t>& in_ids,
                         const std::vector<uint32_t>& out_ids) {
-    DevPlan p;
+    DevPlan p{};
     p.nin = uint32_t(in_ids.size());
     p.nout = uint32_t(out_ids.size());
     p.tab_off = uint32_t(tabs.size());
     p.idx_off = uint32_t(idx.size());
+    p.tab_rows = fixed_rows ? fixed_rows : p.nout;
     for (uint32_t i = 0; i < p.nin; ++i)
-        for (uint32_t r = 0; r < p.nout; ++r) {
+        for (uint32_t r = 0; r < p.tab_rows; ++r) {
             uint32_t t[kTabWords];
-            perm_tables(coefs.at(int(r), int(i)), t);
+            perm_tables(r < p.nout ? coefs.at(int(r), int(i)) : uint8_t(0), t);
             tabs.insert(tabs.end(), t, t + kTabWords);
         }
     idx.insert(idx.end(), in_ids.begin(), in_ids.end());
@@ -68,7 +69,8 @@ uint32_t HostPlans::add(const Mat& coefs, const std::vector<uint32_t>& in_ids,
 }
 
 uint32_t HostPlans::add_noop(uint32_t nin) {
-    DevPlan p{nin, 0, uint32_t(tabs.size()), uint32_t(idx.size())};
+    DevPlan p{nin, 0, uint32_t(tabs.size()), uint32_t(idx.size()), fixed_rows, {0, 0, 0}};
+    tabs.insert(tabs.end(), size_t(nin) * fixed_rows * kTabWords, 0u);
     plans.push_back(p);
     return uint32_t(plans.size() - 1);
 }
@@ -176,7 +178,9 @@ int geom_device(const hec_rs* rs, GeomDevice** out) {
         return HEC_OK;
     }
     std::unique_ptr<GeomDevice> gd(new GeomDevice());
+    const bool is104 = rs->k == 10 && rs->m == 4;
     HostPlans hp;
+    if (is104) hp.fixed_rows = 4;
     Mat par(rs->m, rs->k);
     for (int r = 0; r < rs->m; ++r)
         for (int c = 0; c < rs->k; ++c) par.at(r, c) = rs->matrix.at(rs->k + r, c);
@@ -185,6 +189,7 @@ int geom_device(const hec_rs* rs, GeomDevice** out) {
     for (int j = 0; j < rs->m; ++j) out_ids.push_back(uint32_t(j));
     hp.add(par, in_ids, out_ids);
     if ((rc = gd->encode.upload(hp, nullptr, nullptr))) return rc;
+    gd->encode.fast104 = is104;
     *out = gd.get();
     g_geom[key] = std::move(gd);
     return HEC_OK;
@@ -196,6 +201,8 @@ int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
     const int n = rs->n, k = rs->k;
     if (n > 16) return fail(HEC_ERR_INVALID_ARGUMENT, "device-mask reconstruct needs total shards <= 16");
     HostPlans hp;
+    const bool is104 = k == 10 && rs->m == 4;
+    if (is104) hp.fixed_rows = 4;
     std::vector<uint32_t> lut(size_t(1) << n, kNoPlan);
     const uint32_t noop = hp.add_noop(uint32_t(k));
     uint8_t present[16];
@@ -216,6 +223,7 @@ int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
     }
     int rc = gd->decode_dense.upload(hp, &lut, s);
     if (rc) return rc;
+    gd->decode_dense.fast104 = is104;
     gd->decode_ready = true;
     return HEC_OK;
 }
@@ -239,6 +247,7 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
     a.masks = masks;
     a.lut = ps.lut;
     a.bad_count = bad;
+    a.fast104 = ps.fast104 ? 1u : 0u;
     const uint64_t align = uint64_t(reinterpret_cast<uintptr_t>(in_base)) | in_stripe | in_shard |
                            uint64_t(reinterpret_cast<uintptr_t>(out_base)) | out_stripe | out_shard;
     const bool aligned = (align % 16) == 0;
@@ -401,11 +410,15 @@ const char* hec_last_error_detail(void) { return g_detail.c_str(); }
 
 const char* hec_version(void) { return "libhec 0.1.0 (gfx950)"; }
 
-int hec_set_launch_config(int vec_per_thread, long max_blocks) {
+int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, int blocks_per_cu) {
     if (vec_per_thread != 1 && vec_per_thread != 2 && vec_per_thread != 4)
         return fail(HEC_ERR_INVALID_ARGUMENT, "vec_per_thread must be 1, 2 or 4");
+    if (blocks_per_cu < 0 || blocks_per_cu > 8) return fail(HEC_ERR_INVALID_ARGUMENT, "blocks_per_cu in 0..8");
     launch_config().vec_per_thread = vec_per_thread;
     launch_config().max_blocks = max_blocks < 0 ? 0 : max_blocks;
+    if (xcd_remap < 0) return fail(HEC_ERR_INVALID_ARGUMENT, "xcd_remap >= 0");
+    launch_config().xcd_remap = xcd_remap;
+    launch_config().blocks_per_cu = blocks_per_cu;
     return HEC_OK;
 }
 

@@ -35,6 +35,9 @@ struct HostPlans {
     std::vector<DevPlan> plans;
     std::vector<uint32_t> tabs;
     std::vector<uint32_t> idx;
+    // > 0: every plan (no-ops included) gets exactly nin * fixed_rows table
+    // rows, so plan p's tables start at p * nin * fixed_rows * kTabWords.
+    uint32_t fixed_rows = 0;
     // Append a plan: out rows = coefs (nout x nin) over inputs in_ids.
     uint32_t add(const Mat& coefs, const std::vector<uint32_t>& in_ids,
                  const std::vector<uint32_t>& out_ids);
@@ -48,6 +51,7 @@ struct DevicePlanSet {
     uint32_t* idx = nullptr;
     uint32_t* lut = nullptr;
     size_t cap_plans = 0, cap_tabs = 0, cap_idx = 0, cap_lut = 0;
+    bool fast104 = false;  // RS(10,4) set with fixed 4-row tables (rs104_kernel eligible)
     int upload(const HostPlans& hp, const std::vector<uint32_t>* lut_host, hipStream_t s);
     void release();
 };

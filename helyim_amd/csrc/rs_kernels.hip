@@ -165,7 +165,15 @@ __device__ __forceinline__ void apply_group(const ApplyArgs& a, const uint8_t* i
 
 template <int K, int U, bool ALIGNED, bool XORONLY = false>
 __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
-    for (uint64_t item = blockIdx.x; item < a.n_items; item += gridDim.x) {
+    // XCD-aware chunk mapping: workgroups b, b+8, b+16, ... are dealt to one
+    // XCD (MI355X_MICROARCH.md, dispatch), so a bijective remap hands them
+    // consecutive chunks. Speed only: correctness never depends on placement.
+    uint64_t first = blockIdx.x;
+    if (a.xcd_remap) {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blockIdx.x % 8;
+        first = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
+    }
+    for (uint64_t item = first; item < a.n_items; item += gridDim.x) {
         const uint32_t stripe = uint32_t(item / a.chunks_per_stripe);
         const uint32_t chunk = uint32_t(item - uint64_t(stripe) * a.chunks_per_stripe);
         uint32_t pid = 0;
@@ -177,14 +185,14 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
             }
         }
         const __attribute__((address_space(4))) DevPlan* pp = as_const(a.plans) + pid;
-        const DevPlan p{pp->nin, pp->nout, pp->tab_off, pp->idx_off};
+        const DevPlan p{pp->nin, pp->nout, pp->tab_off, pp->idx_off, pp->tab_rows, {0, 0, 0}};
         if (p.nout == 0) continue;
         const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
         uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
         cu32p in_ids = as_const(a.idx) + p.idx_off;
         cu32p out_ids = in_ids + p.nin;
         cu32p tab = as_const(a.tabs) + p.tab_off;
-        const uint32_t row_stride = p.nout * 5;  // words per input
+        const uint32_t row_stride = p.tab_rows * 5;  // words per input
         const uint64_t chunk_off = uint64_t(chunk) * (uint64_t(U) * kThreads * kVecBytes);
         for (uint32_t g = 0; g < p.nout; g += 4) {
             const uint32_t R = p.nout - g < 4 ? p.nout - g : 4;
@@ -199,6 +207,113 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// RS(10,4) fast paths (k = 10, n = 14, 16-byte aligned strides): the shard ids
+// come from kernel arguments (encode) or straight from the stripe's present
+// mask with scalar bit scans (decode), so a workgroup issues its ten 16-byte
+// loads after at most ONE scalar load; the coefficient tables (fixed stride
+// of 4 rows x 5 words per input) arrive in parallel with the data.
+// ---------------------------------------------------------------------------
+// Workgroup -> chunk mapping. Workgroups b, b+8, b+16, ... are dealt to one
+// XCD (observed round-robin dispatch; MI355X_MICROARCH.md), so:
+//   mode 0: identity;
+//   mode 1: XCD x takes the contiguous x-th eighth of all chunks;
+//   mode G >= 2: XCD x takes runs of G consecutive chunks, XCDs interleaved
+//               run by run (applied to the largest prefix divisible by 8G).
+// Always a bijection; speed only, never correctness.
+__device__ __forceinline__ uint32_t remap_block(uint32_t b, uint32_t nb, uint32_t mode) {
+    if (mode == 0) return b;
+    const uint32_t x = b % 8, j = b / 8;
+    if (mode == 1) {
+        const uint32_t q = nb / 8, r = nb % 8;
+        return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+    }
+    const uint32_t full = nb / (8 * mode) * (8 * mode);
+    if (b >= full) return b;
+    return (j / mode) * (8 * mode) + x * mode + (j % mode);
+}
+
+template <bool DEC, bool XORONLY>
+__global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
+    constexpr int K = 10, N = 14, R = 4;
+    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap);
+    const uint32_t stripe = item / a.chunks_per_stripe;
+    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
+    uint32_t in_id[K], out_id[R];
+    uint32_t nout = R;
+    cu32p tab = as_const(a.tabs);
+    if constexpr (DEC) {
+        const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
+        const uint32_t present = __builtin_popcount(mask);
+        if (present < K) {
+            if (chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
+            return;
+        }
+        if (present == N) return;  // upstream: all present -> no-op
+        nout = N - present;
+        uint32_t m = mask;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {  // first K present shards, ascending
+            in_id[i] = __builtin_ctz(m);
+            m &= m - 1;
+        }
+        uint32_t e = ~mask & ((1u << N) - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {  // erased shards, ascending
+            out_id[r] = e ? __builtin_ctz(e) : 0;
+            e &= e - 1;
+        }
+        tab += as_const(a.lut)[mask] * (K * R * 5);
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) in_id[i] = i;
+#pragma unroll
+        for (int r = 0; r < R; ++r) out_id[r] = r;
+    }
+    const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
+    uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
+    const uint64_t o = uint64_t(chunk) * (kThreads * kVecBytes) + threadIdx.x * kVecBytes;
+    if (o >= a.len) return;
+    const uint64_t avail = a.len - o;
+    u32x4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+    if (avail >= kVecBytes) {
+        u32x4 d[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) d[i] = load_full(in_b + uint64_t(in_id[i]) * a.in_shard + o, true);
+#pragma unroll
+        for (int i = 0; i < K; ++i) mac<R, XORONLY>(acc, d[i], tab + i * (R * 5));
+        // Materialise every row before the uniform `r < nout` store branches:
+        // otherwise the compiler sinks each row's math into its branch, keeps
+        // all 200 table words live and spills SGPRs (154 VGPRs, 3 waves/SIMD).
+#pragma unroll
+        for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r < int(nout)) store_full(out_b + uint64_t(out_id[r]) * a.out_shard + o, acc[r], true);
+    } else {
+        for (int i = 0; i < K; ++i) {
+            const u32x4 d = load_tail(in_b + uint64_t(in_id[i]) * a.in_shard + o, avail);
+            gf_mac<R>(acc, d, tab + i * (R * 5));
+        }
+        for (int r = 0; r < R; ++r)
+            if (r < int(nout)) store_tail(out_b + uint64_t(out_id[r]) * a.out_shard + o, acc[r], avail);
+    }
+}
+
+template <bool DEC, bool XORONLY>
+static hipError_t launch_rs104(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
+    const uint64_t chunk = uint64_t(kThreads) * kVecBytes;
+    a.chunks_per_stripe = uint32_t((a.len + chunk - 1) / chunk);
+    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
+    if (a.n_items == 0) return hipSuccess;
+    a.xcd_remap = uint32_t(cfg.xcd_remap);
+    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
+    hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY>), dim3(uint32_t(a.n_items)), dim3(kThreads), lds, stream, a);
+    return hipGetLastError();
+}
+
 template <int K, int U, bool ALIGNED, bool XORONLY = false>
 static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
     const uint64_t chunk = uint64_t(U) * kThreads * kVecBytes;
@@ -208,12 +323,22 @@ static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t str
     uint64_t grid = a.n_items;
     if (cfg.max_blocks > 0 && grid > uint64_t(cfg.max_blocks)) grid = uint64_t(cfg.max_blocks);
     if (grid > 0x7FFFFFFFull) grid = 0x7FFFFFFFull;
-    hipLaunchKernelGGL((rs_apply_kernel<K, U, ALIGNED, XORONLY>), dim3(uint32_t(grid)), dim3(kThreads), 0, stream, a);
+    a.xcd_remap = cfg.xcd_remap ? 1u : 0u;
+    // Occupancy cap: dynamic LDS that only blocks_per_cu workgroups fit in 160 KiB.
+    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
+    hipLaunchKernelGGL((rs_apply_kernel<K, U, ALIGNED, XORONLY>), dim3(uint32_t(grid)), dim3(kThreads), lds, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
                         hipStream_t stream) {
+    // RS(10,4) fast path: fixed 4-row table stride, one 4 KiB chunk per workgroup.
+    const uint64_t items = ((a.len + 4095) / 4096) * a.n_stripes;
+    if (a.fast104 && aligned && cfg.vec_per_thread == 1 && cfg.max_blocks == 0 && items < 0x7FFFFFFFull) {
+        if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, cfg, stream)
+                                          : launch_rs104<true, false>(a, cfg, stream);
+        return cfg.mode == 1 ? launch_rs104<false, true>(a, cfg, stream) : launch_rs104<false, false>(a, cfg, stream);
+    }
     if (nin == 10 && aligned && cfg.mode == 1) {
         switch (cfg.vec_per_thread) {
             case 1: return launch_t<10, 1, true, true>(a, cfg, stream);

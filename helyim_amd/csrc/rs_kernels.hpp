@@ -13,8 +13,10 @@ namespace hec {
 struct DevPlan {
     uint32_t nin;      // inputs (== data shard count)
     uint32_t nout;     // outputs; 0 = nothing to do (all shards present)
-    uint32_t tab_off;  // word offset of this plan's tables: [nin][nout][kTabWords]
+    uint32_t tab_off;  // word offset of this plan's tables: [nin][tab_rows][kTabWords]
     uint32_t idx_off;  // word offset of [nin] input shard ids then [nout] output ids
+    uint32_t tab_rows; // table row stride (>= nout; padded rows hold coefficient 0)
+    uint32_t pad[3];
 };
 
 constexpr uint32_t kNoPlan = 0xFFFFFFFFu;   // mask LUT entry: too few shards present
@@ -38,12 +40,17 @@ struct ApplyArgs {
     const uint32_t* masks;       // optional per-stripe present mask (bit i = shard i present)
     const uint32_t* lut;         // mask -> plan id (used when masks != nullptr)
     uint32_t* bad_count;         // optional: stripes skipped for too few present shards
+    uint32_t xcd_remap;          // 1: workgroups sharing an XCD take consecutive chunks
+    uint32_t fast104;            // 1: RS(10,4) plan set with 4-row tables; encode = plan 0 at
+                                 //    offset 0, decode = tables at lut[mask] * 200 words
 };
 
 struct LaunchConfig {
     int vec_per_thread = 1;      // 16-byte vectors per lane per chunk (1, 2 or 4)
     long max_blocks = 0;         // grid cap (0 = one block per chunk)
     int mode = 0;                // 0 = GF coding; 1 = XOR-only bandwidth ceiling (diagnostic)
+    int xcd_remap = 1;           // 0 none, 1 eighths, G>=2 runs of G chunks per XCD (speed only)
+    int blocks_per_cu = 0;       // >0: cap resident workgroups per CU via dynamic LDS (0 = no cap)
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees

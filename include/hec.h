@@ -177,9 +177,13 @@ int hec_write_ec_files_ex(const char* base_filename, uint64_t buf_size, uint64_t
 int hec_rebuild_ec_files(const char* base_filename, uint32_t* rebuilt_ids, size_t* n_rebuilt);
 
 /* ---- tuning / introspection ----------------------------------------------- */
-/* Kernel launch configuration: 16-byte vectors per lane per chunk (1, 2, 4)
- * and grid cap (0 = one workgroup per chunk). Returns previous values. */
-int hec_set_launch_config(int vec_per_thread, long max_blocks);
+/* Kernel launch configuration (process-wide; speed only, results identical):
+ * vec_per_thread 16-byte vectors per lane per chunk (1, 2, 4); max_blocks
+ * grid cap (0 = one workgroup per 4 KiB chunk); xcd_remap: 0 none, 1 = the
+ * workgroups of one XCD take a contiguous eighth of the chunks, G >= 2 = runs
+ * of G consecutive chunks per XCD; blocks_per_cu > 0 caps resident
+ * workgroups per CU (0 = no cap). */
+int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, int blocks_per_cu);
 /* Diagnostic: 0 = GF(2^8) coding (default); 1 = XOR-only bandwidth ceiling --
  * the RS(10,4) aligned kernel with its GF math replaced by plain XOR (same
  * loads, stores and addressing; WRONG parity by design), used only to measure

@@ -116,25 +116,41 @@ def test_batch_encode_vs_oracle(gpu, L):
     assert np.array_equal(host[:, 10:], ref)
 
 
-@pytest.mark.parametrize("vec", [1, 2, 4])
-@pytest.mark.parametrize("max_blocks", [0, 97])
-def test_launch_configs_identical(gpu, vec, max_blocks):
+@pytest.mark.parametrize("vec,max_blocks,remap,bpc", [
+    (1, 0, 0, 0), (1, 0, 1, 0), (1, 0, 16, 0), (1, 0, 256, 3), (1, 97, 1, 0),
+    (2, 0, 1, 0), (2, 97, 0, 0), (4, 0, 64, 0), (4, 97, 1, 2)])
+def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc):
+    """Every launch configuration (fast and generic kernels, XCD remaps,
+    occupancy caps) produces identical encode and decode bytes."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rs = H.ReedSolomon(10, 4)
-    S, L = 9, 3 * 8192 + 48
+    S, L = 37, 3 * 8192 + 48
     t = _stripes(S, L)
+    B.set_launch_config()
     ref = t.clone()
-    B.set_launch_config(1, 0)
     B.encode_batch(rs, ref)
+    rng = np.random.default_rng(vec * 1000 + remap)
+    masks = np.array([((1 << 14) - 1) & ~int(sum(1 << int(i) for i in rng.choice(14, int(rng.integers(0, 5)),
+                                                                                 replace=False)))
+                      for _ in range(S)], dtype=np.int32)
     try:
-        B.set_launch_config(vec, max_blocks)
+        B.set_launch_config(vec, max_blocks, remap, bpc)
         B.encode_batch(rs, t)
+        torch.cuda.synchronize()
+        assert torch.equal(t, ref)
+        er = torch.zeros((S, 14), dtype=torch.bool)
+        for s in range(S):
+            for i in range(14):
+                er[s, i] = not (masks[s] >> i) & 1
+        er = er.cuda()
+        t[er] = 0
+        B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(t, ref)
     finally:
-        B.set_launch_config(1, 0)
-    torch.cuda.synchronize()
-    assert torch.equal(t, ref)
+        B.set_launch_config()
 
 
 def test_batch_encode_separate_and_unaligned(gpu):

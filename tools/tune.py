@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--vecs", default="1,2,4")
     ap.add_argument("--blocks", default="0,2048,4096,8192")
     ap.add_argument("--modes", default="0,1")
+    ap.add_argument("--remaps", default="1")
+    ap.add_argument("--bpcs", default="0", help="blocks-per-CU caps (0 = none)")
     ap.add_argument("--pad", type=int, default=0, help="extra bytes between shards (breaks 2^20 strides)")
     ap.add_argument("--tile", type=int, default=0,
                     help="interleaved layout: every shard split in tiles of this many bytes, the 14 "
@@ -46,16 +48,16 @@ def main():
     B.encode_batch(rs, t)
     torch.cuda.synchronize()
     good = t[:8].clone()
-    configs = [(mode, v, b) for mode in [int(x) for x in args.modes.split(",")]
-               for v, b in itertools.product([int(x) for x in args.vecs.split(",")],
-                                             [int(x) for x in args.blocks.split(",")])]
+    ints = lambda x: [int(y) for y in x.split(",")]
+    configs = list(itertools.product(ints(args.modes), ints(args.vecs), ints(args.blocks), ints(args.remaps),
+                                     ints(args.bpcs)))
     res = {c: {"enc": [], "dec": []} for c in configs}
     s = torch.cuda.current_stream()
     for _ in range(args.rounds):
         for c in configs:
-            mode, v, b = c
+            mode, v, b, rm, bpc = c
             H.lib.hec_set_kernel_mode(mode)
-            B.set_launch_config(v, b)
+            B.set_launch_config(v, b, rm, bpc)
             e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             e0.record(s)
             B.encode_batch(rs, t)
@@ -66,12 +68,13 @@ def main():
             res[c]["enc"].append(e0.elapsed_time(e1))
             res[c]["dec"].append(e1.elapsed_time(e2))
     H.lib.hec_set_kernel_mode(0)
-    B.set_launch_config(1, 0)
+    B.set_launch_config()
     nbytes = S * 14 * L
     for c in configs:
         enc, dec = np.array(res[c]["enc"]), np.array(res[c]["dec"])
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "pad": args.pad, "tile": args.tile,
                           "mode": ["gf", "xor_ceiling"][c[0]], "vec_per_thread": c[1], "max_blocks": c[2],
+                          "xcd_remap": c[3], "blocks_per_cu": c[4],
                           "enc_ms_med": round(float(np.median(enc)), 3), "enc_ms_min": round(float(enc.min()), 3),
                           "enc_GBps": round(nbytes / np.median(enc) / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 3),

@@ -18,21 +18,38 @@ import sys
 
 
 def load(path, counter):
+    """-> {kernel name: [bytes per full-grid dispatch, ...]}"""
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     full = max(int(r["Grid_Size"]) for r in rows)
     rows = [r for r in rows if int(r["Grid_Size"]) == full]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    return [float(r["Counter_Value"]) * 1024 for r in rows], rows[0]["Kernel_Name"], full
+    out = {}
+    for r in rows:
+        out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]) * 1024)
+    return out, full
+
+
+def split(per_kernel):
+    """encode / decode series: rs104_kernel<false,...> / <true,...>; a single
+    generic kernel alternates encode (even) / decode (odd)."""
+    enc = [v for k, v in per_kernel.items() if "rs104_kernel<false" in k]
+    dec = [v for k, v in per_kernel.items() if "rs104_kernel<true" in k]
+    if enc and dec:
+        return enc[0], dec[0], sorted(per_kernel)
+    (k, v), = per_kernel.items()
+    return v[0::2], v[1::2], [k]
 
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    fetch, kname, grid = load(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write, _, _ = load(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    enc_r = statistics.median(fetch[0::2]) * 2
-    dec_r = statistics.median(fetch[1::2]) * 2
-    enc_w = statistics.median(write[0::2])
-    dec_w = statistics.median(write[1::2])
+    fetch, grid = load(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write, _ = load(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    fe, fd, kname = split(fetch)
+    we, wd, _ = split(write)
+    enc_r = statistics.median(fe) * 2
+    dec_r = statistics.median(fd) * 2
+    enc_w = statistics.median(we)
+    dec_w = statistics.median(wd)
     S, L = 4096, 1 << 20
     out = {
         "source": src,

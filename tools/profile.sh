@@ -9,8 +9,8 @@ export TMPDIR=/tmp
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras > $OUT/bench_trace.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex rs_apply --output-format csv \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex "rs104|rs_apply" --output-format csv \
     -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --kernel-include-regex rs_apply --output-format csv \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --kernel-include-regex "rs104|rs_apply" --output-format csv \
     -d $OUT/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_write.log 2>&1
 find $OUT -name "*.csv" | sort

@@ -6,17 +6,29 @@
 // blocks while anything remains, encoder.rs:228), short reads zero-filled
 // (encoder.rs:169-189), shard file j = concatenation of block j of every row.
 // The reference's 256 KiB buffer only sets its I/O granularity (bytes are
-// position-wise independent), so here whole batches of rows go through the
-// GPU at once: pread -> pinned host -> H2D -> kernel -> D2H -> pwrite.
+// position-wise independent), so whole batches of rows go through the GPU.
+//
+// Pipeline (3 slots): for job k the main thread preads (parallel pieces on an
+// I/O pool) into slot k%3's pinned buffer, then queues H2D -> kernel -> D2H on
+// the slot's stream; a writer thread waits for the slot's event and pwritev()s
+// all 14 (or the rebuilt) shard files in parallel on the pool. Reading job
+// k+1, the GPU work of job k and the writes of job k-1 overlap.
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
 #include <string>
+#include <thread>
 
 #include "hec_internal.hpp"
 
@@ -24,16 +36,16 @@ namespace hec {
 namespace {
 
 constexpr int K = 10, M = 4, N = 14;
-constexpr uint64_t kBatchBytes = 256ull << 20;  // data bytes per GPU batch
+constexpr int kSlots = 3;
+constexpr uint64_t kBatchBytes = 256ull << 20;  // data bytes per GPU job
 constexpr uint64_t kLargeSlice = 16ull << 20;   // per-shard slice of a large row
+constexpr int kIoThreads = 16;
 
 std::string shard_name(const std::string& base, int i) {
     char ext[8];
     std::snprintf(ext, sizeof ext, ".ec%02d", i);  // to_ext, helyim-ec/src/lib.rs:84-86
     return base + ext;
 }
-
-int io_fail(const std::string& what) { return fail(HEC_ERR_IO, what + ": " + std::strerror(errno)); }
 
 struct Fd {
     int fd = -1;
@@ -42,47 +54,312 @@ struct Fd {
     }
 };
 
-struct Pinned {
-    uint8_t* p = nullptr;
-    ~Pinned() {
-        if (p) (void)hipHostFree(p);
+// ---------------------------------------------------------------------------
+// First-error record shared by the pipeline's threads.
+// ---------------------------------------------------------------------------
+struct ErrorSlot {
+    std::mutex mu;
+    std::atomic<int> code{HEC_OK};
+    std::string detail;
+    void set(int c, const std::string& d) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (code.load() == HEC_OK) {
+            detail = d;
+            code.store(c);
+        }
     }
+    bool failed() const { return code.load() != HEC_OK; }
 };
 
-struct DevBuf {
-    uint8_t* p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
+void io_error(ErrorSlot& e, const std::string& what) { e.set(HEC_ERR_IO, what + ": " + std::strerror(errno)); }
+
+// ---------------------------------------------------------------------------
+// Small fixed thread pool with fork/join task groups.
+// ---------------------------------------------------------------------------
+class Pool {
+   public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
     }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // Run all tasks, return when every one finished.
+    void run_all(std::vector<std::function<void()>>& tasks) {
+        if (tasks.empty()) return;
+        std::mutex dm;
+        std::condition_variable dcv;
+        size_t left = tasks.size();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (auto& t : tasks)
+                q_.push_back([&, fn = std::move(t)] {
+                    fn();
+                    std::lock_guard<std::mutex> l2(dm);
+                    if (--left == 0) dcv.notify_all();
+                });
+        }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> lk(dm);
+        dcv.wait(lk, [&] { return left == 0; });
+        tasks.clear();
+    }
+
+   private:
+    void loop() {
+        for (;;) {
+            std::function<void()> fn;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                fn = std::move(q_.front());
+                q_.pop_front();
+            }
+            fn();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::deque<std::function<void()>> q_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false;
 };
 
 // pread that loops over short reads and zero-fills past EOF (encoder.rs:169-189).
-int pread_zero(int fd, uint8_t* dst, uint64_t len, uint64_t off) {
+bool pread_zero(int fd, uint8_t* dst, uint64_t len, uint64_t off, ErrorSlot& e) {
     uint64_t got = 0;
     while (got < len) {
         ssize_t r = ::pread(fd, dst + got, len - got, off_t(off + got));
         if (r < 0) {
             if (errno == EINTR) continue;
-            return io_fail("read");
+            io_error(e, "read");
+            return false;
         }
         if (r == 0) break;
         got += uint64_t(r);
     }
     if (got < len) std::memset(dst + got, 0, len - got);
-    return HEC_OK;
+    return true;
 }
 
-int pwrite_all(int fd, const uint8_t* src, uint64_t len, uint64_t off) {
-    uint64_t put = 0;
-    while (put < len) {
-        ssize_t w = ::pwrite(fd, src + put, len - put, off_t(off + put));
+// pwritev of a gather list at a file offset, looping over short writes.
+bool pwritev_all(int fd, std::vector<iovec> iov, uint64_t off, ErrorSlot& e) {
+    size_t first = 0;
+    while (first < iov.size()) {
+        const int cnt = int(std::min<size_t>(iov.size() - first, 1024));
+        ssize_t w = ::pwritev(fd, iov.data() + first, cnt, off_t(off));
         if (w < 0) {
             if (errno == EINTR) continue;
-            return io_fail("write");
+            io_error(e, "write");
+            return false;
         }
-        put += uint64_t(w);
+        off += uint64_t(w);
+        while (w > 0 && first < iov.size()) {
+            if (size_t(w) >= iov[first].iov_len) {
+                w -= ssize_t(iov[first].iov_len);
+                ++first;
+            } else {
+                iov[first].iov_base = static_cast<uint8_t*>(iov[first].iov_base) + w;
+                iov[first].iov_len -= size_t(w);
+                w = 0;
+            }
+        }
     }
-    return HEC_OK;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// One unit of pipelined work.
+// ---------------------------------------------------------------------------
+struct ReadSeg {
+    int fd;
+    uint64_t host_off, len, file_off;
+};
+struct WriteSeg {
+    int fd;
+    uint64_t file_off;
+    std::vector<std::pair<uint64_t, uint64_t>> pieces;  // (host_off, len) in order
+};
+struct Copy {
+    uint64_t host_off, dev_off, len;
+};
+struct Job {
+    std::vector<ReadSeg> reads;
+    std::vector<Copy> h2d, d2h;
+    std::function<int(uint8_t* dev, hipStream_t)> kernel;
+    std::vector<WriteSeg> writes;
+};
+
+struct Slot {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+};
+
+// Persistent per-device pipeline (one per GPU, reused by every file call so
+// small volumes do not pay for pinned allocation, streams and threads).
+class FilePipeline {
+   public:
+    FilePipeline() : pool_(kIoThreads) {}
+    // Grow the slots to at least these sizes; call only while idle.
+    int ensure(uint64_t host_bytes, uint64_t dev_bytes) {
+        HEC_HIP(hipGetDevice(&dev_id_));
+        for (auto& s : slots_) {
+            if (!s.stream) {
+                HEC_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+                HEC_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+            }
+            if (host_bytes > host_cap_) {
+                if (s.host) HEC_HIP(hipHostFree(s.host));
+                s.host = nullptr;
+                HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.host), host_bytes, hipHostMallocDefault));
+            }
+            if (dev_bytes > dev_cap_) {
+                if (s.dev) HEC_HIP(hipFree(s.dev));
+                s.dev = nullptr;
+                HEC_HIP(hipMalloc(reinterpret_cast<void**>(&s.dev), dev_bytes));
+            }
+        }
+        host_cap_ = std::max(host_cap_, host_bytes);
+        dev_cap_ = std::max(dev_cap_, dev_bytes);
+        if (!writer_.joinable()) writer_ = std::thread([this] { writer_loop(); });
+        return HEC_OK;
+    }
+    // Submit one job (blocks while its slot is still being written).
+    void submit(Job job) {
+        if (err_.failed()) return;
+        const int si = int(next_++ % kSlots);
+        Slot& s = slots_[si];
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return !s.busy; });
+            s.busy = true;
+            ++inflight_;
+        }
+        if (err_.failed()) return release(si);
+        // reads in parallel pieces
+        std::vector<std::function<void()>> tasks;
+        for (const ReadSeg& r : job.reads)
+            tasks.push_back([this, &s, r] {
+                if (!err_.failed()) pread_zero(r.fd, s.host + r.host_off, r.len, r.file_off, err_);
+            });
+        pool_.run_all(tasks);
+        if (err_.failed()) return release(si);
+        int rc = gpu(s, job);
+        if (rc) {
+            err_.set(rc, hec_last_error_detail());
+            return release(si);
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            wq_.emplace_back(si, std::move(job));
+        }
+        cv_.notify_all();
+    }
+    // Wait until every submitted job is written; return (and clear) the first error.
+    int drain() {
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [this] { return inflight_ == 0; });
+        }
+        int code = err_.code.load();
+        std::string detail = err_.detail;
+        err_.code.store(HEC_OK);
+        err_.detail.clear();
+        return code ? fail(code, detail) : HEC_OK;
+    }
+    ErrorSlot& errors() { return err_; }
+
+   private:
+    int gpu(Slot& s, const Job& job) {
+        for (const Copy& c : job.h2d)
+            HEC_HIP(hipMemcpyAsync(s.dev + c.dev_off, s.host + c.host_off, c.len, hipMemcpyHostToDevice, s.stream));
+        int rc = job.kernel(s.dev, s.stream);
+        if (rc) return rc;
+        for (const Copy& c : job.d2h)
+            HEC_HIP(hipMemcpyAsync(s.host + c.host_off, s.dev + c.dev_off, c.len, hipMemcpyDeviceToHost, s.stream));
+        HEC_HIP(hipEventRecord(s.done, s.stream));
+        return HEC_OK;
+    }
+    void release(int si) {
+        std::lock_guard<std::mutex> lk(mu_);
+        slots_[si].busy = false;
+        --inflight_;
+        cv_.notify_all();
+    }
+    void writer_loop() {
+        (void)hipSetDevice(dev_id_);
+        for (;;) {
+            std::pair<int, Job> w;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return !wq_.empty(); });
+                w = std::move(wq_.front());
+                wq_.pop_front();
+            }
+            Slot& s = slots_[w.first];
+            hipError_t he = hipEventSynchronize(s.done);
+            if (he != hipSuccess) err_.set(HEC_ERR_HIP, std::string("hipEventSynchronize: ") + hipGetErrorString(he));
+            if (!err_.failed()) {
+                std::vector<std::function<void()>> tasks;
+                for (const WriteSeg& ws : w.second.writes)
+                    tasks.push_back([this, &s, &ws] {
+                        if (err_.failed()) return;
+                        std::vector<iovec> iov;
+                        for (auto& p : ws.pieces) iov.push_back(iovec{s.host + p.first, p.second});
+                        pwritev_all(ws.fd, std::move(iov), ws.file_off, err_);
+                    });
+                pool_.run_all(tasks);
+            }
+            release(w.first);
+        }
+    }
+
+    Pool pool_;
+    Slot slots_[kSlots];
+    std::thread writer_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::pair<int, Job>> wq_;
+    uint64_t inflight_ = 0;
+    uint64_t host_cap_ = 0, dev_cap_ = 0;
+    uint64_t next_ = 0;
+    int dev_id_ = 0;
+    ErrorSlot err_;
+};
+
+// One pipeline per device, created on first use and intentionally never
+// destroyed (its threads and HIP resources live for the process; a static
+// destructor could run after the HIP runtime is gone).
+struct PipelineLease {
+    std::unique_lock<std::mutex> lock;
+    FilePipeline* pipe = nullptr;
+};
+int lease_pipeline(uint64_t host_bytes, uint64_t dev_bytes, PipelineLease& out) {
+    static std::mutex reg_mu;
+    static std::map<int, std::pair<std::mutex*, FilePipeline*>>* reg =
+        new std::map<int, std::pair<std::mutex*, FilePipeline*>>();
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    std::pair<std::mutex*, FilePipeline*> e;
+    {
+        std::lock_guard<std::mutex> lk(reg_mu);
+        auto& slot = (*reg)[dev];
+        if (!slot.first) slot = {new std::mutex(), new FilePipeline()};
+        e = slot;
+    }
+    out.lock = std::unique_lock<std::mutex>(*e.first);  // one file operation per device at a time
+    out.pipe = e.second;
+    return e.second->ensure(host_bytes, dev_bytes);
 }
 
 struct Rs104 {
@@ -90,15 +367,23 @@ struct Rs104 {
     ~Rs104() { hec_rs_free(rs); }
 };
 
+// Split [off, off+len) into up to `parts` read pieces of whole `unit`s.
+void add_reads(std::vector<ReadSeg>& v, int fd, uint64_t host_off, uint64_t len, uint64_t file_off, uint64_t unit,
+               int parts) {
+    uint64_t units = (len + unit - 1) / unit;
+    uint64_t per = std::max<uint64_t>(1, (units + parts - 1) / parts) * unit;
+    for (uint64_t o = 0; o < len; o += per) v.push_back({fd, host_off + o, std::min(per, len - o), file_off + o});
+}
+
 }  // namespace
 
 static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint64_t large, uint64_t small) {
     // generate_ec_files: open .dat read-only (encoder.rs:58-62)
     Fd dat;
     dat.fd = ::open((base + ".dat").c_str(), O_RDONLY);
-    if (dat.fd < 0) return io_fail("open " + base + ".dat");
+    if (dat.fd < 0) return fail(HEC_ERR_IO, "open " + base + ".dat: " + std::strerror(errno));
     struct stat st;
-    if (::fstat(dat.fd, &st) != 0) return io_fail("stat .dat");
+    if (::fstat(dat.fd, &st) != 0) return fail(HEC_ERR_IO, std::string("stat .dat: ") + std::strerror(errno));
     int64_t remaining = int64_t(st.st_size);
 
     Rs104 rs;  // ReedSolomon::new(10, 4) (encoder.rs:208-209)
@@ -109,50 +394,48 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     Fd out[N];  // open_ec_files(base, false): create + truncate (encoder.rs:111-127)
     for (int i = 0; i < N; ++i) {
         out[i].fd = ::open(shard_name(base, i).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        if (out[i].fd < 0) return io_fail("open " + shard_name(base, i));
+        if (out[i].fd < 0) return fail(HEC_ERR_IO, "open " + shard_name(base, i) + ": " + std::strerror(errno));
     }
+    const uint64_t large_row = large * K, small_row = small * K;
+    // the reference checks block % buf at the first row of each kind (encoder.rs:139-144)
+    const bool has_large = remaining > int64_t(large_row);
+    if (has_large && large % buf_size != 0)
+        return fail(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
+                    "unexpected block size " + std::to_string(large) + ", buffer size " + std::to_string(buf_size));
+    // rows of each kind, to size the staging buffers no larger than needed
+    const uint64_t n_large = has_large ? (uint64_t(remaining) - 1) / large_row : 0;
+    const int64_t small_bytes = remaining - int64_t(n_large * large_row);
+    const uint64_t n_small = small_bytes > 0 ? (uint64_t(small_bytes) + small_row - 1) / small_row : 0;
     GeomDevice* gd;
     if ((rc = geom_device(rs.rs, &gd))) return rc;
-    hipStream_t s;
-    HEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    struct StreamGuard {
-        hipStream_t s;
-        ~StreamGuard() { (void)hipStreamDestroy(s); }
-    } sg{s};
 
-    // Host/device staging sized for one batch (whole small rows, or a slice
-    // of one large row).
-    const uint64_t per_shard_cap = std::max<uint64_t>(small, std::min<uint64_t>(large, kLargeSlice));
-    uint64_t small_rows_per_batch = std::max<uint64_t>(1, kBatchBytes / (uint64_t(K) * small));
-    uint64_t data_cap = std::max<uint64_t>(per_shard_cap * K, small_rows_per_batch * K * small);
-    Pinned hdata, hpar;
-    DevBuf ddata, dpar;
-    HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&hdata.p), data_cap, hipHostMallocDefault));
-    HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&hpar.p), data_cap / K * M, hipHostMallocDefault));
-    HEC_HIP(hipMalloc(reinterpret_cast<void**>(&ddata.p), data_cap));
-    HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dpar.p), data_cap / K * M));
+    const uint64_t T = n_large ? std::min<uint64_t>(large, kLargeSlice) : 0;                    // large-row slice
+    const uint64_t B = std::min(n_small, std::max<uint64_t>(1, kBatchBytes / small_row));  // small rows per job
+    const uint64_t data_cap = (std::max(T * K, B * small_row) + 255) / 256 * 256;
+    const uint64_t par_cap = std::max<uint64_t>(256, std::max(T * M, B * small * M));
+    PipelineLease lease;
+    if ((rc = lease_pipeline(data_cap + par_cap, data_cap + par_cap, lease))) return rc;
+    FilePipeline& pipe = *lease.pipe;
+    const DevicePlanSet* enc = &gd->encode;
 
-    uint64_t out_off = 0;      // current size of every shard file
-    uint64_t processed = 0;    // .dat offset of the current row
-    const uint64_t large_row = large * K, small_row = small * K;
+    uint64_t out_off = 0;    // current size of every shard file
+    uint64_t processed = 0;  // .dat offset of the current row
 
     // Large rows (encoder.rs:215-226): block j of the row = .dat[row + j*large, +large)
-    while (remaining > int64_t(large_row)) {
-        if (large % buf_size != 0) return fail(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
-                                               "unexpected block size " + std::to_string(large) +
-                                                   ", buffer size " + std::to_string(buf_size));
-        for (uint64_t t = 0; t < large; t += per_shard_cap) {
-            const uint64_t T = std::min(per_shard_cap, large - t);
+    while (remaining > int64_t(large_row) && !pipe.errors().failed()) {
+        for (uint64_t t = 0; t < large; t += T) {
+            const uint64_t n = std::min(T, large - t);
+            Job job;
             for (int j = 0; j < K; ++j)
-                if ((rc = pread_zero(dat.fd, hdata.p + j * T, T, processed + j * large + t))) return rc;
-            HEC_HIP(hipMemcpyAsync(ddata.p, hdata.p, T * K, hipMemcpyHostToDevice, s));
-            if ((rc = run_apply(gd->encode, K, ddata.p, 0, T, dpar.p, 0, T, T, 1, nullptr, nullptr, s))) return rc;
-            HEC_HIP(hipMemcpyAsync(hpar.p, dpar.p, T * M, hipMemcpyDeviceToHost, s));
-            HEC_HIP(hipStreamSynchronize(s));
-            for (int j = 0; j < K; ++j)
-                if ((rc = pwrite_all(out[j].fd, hdata.p + j * T, T, out_off + t))) return rc;
-            for (int j = 0; j < M; ++j)
-                if ((rc = pwrite_all(out[K + j].fd, hpar.p + j * T, T, out_off + t))) return rc;
+                add_reads(job.reads, dat.fd, j * n, n, processed + j * large + t, 1 << 20, 2);
+            job.h2d.push_back({0, 0, n * K});
+            job.kernel = [=](uint8_t* d, hipStream_t s) {
+                return run_apply(*enc, K, d, 0, n, d + data_cap, 0, n, n, 1, nullptr, nullptr, s);
+            };
+            job.d2h.push_back({data_cap, data_cap, n * M});
+            for (int j = 0; j < K; ++j) job.writes.push_back({out[j].fd, out_off + t, {{j * n, n}}});
+            for (int j = 0; j < M; ++j) job.writes.push_back({out[K + j].fd, out_off + t, {{data_cap + j * n, n}}});
+            pipe.submit(std::move(job));
         }
         out_off += large;
         processed += large_row;
@@ -160,32 +443,36 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     }
 
     // Small rows (encoder.rs:228-239): whole rows are contiguous in .dat.
-    while (remaining > 0) {
-        if (small % buf_size != 0) return fail(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
-                                               "unexpected block size " + std::to_string(small) +
-                                                   ", buffer size " + std::to_string(buf_size));
-        const uint64_t rows_left = (uint64_t(remaining) + small_row - 1) / small_row;
-        const uint64_t B = std::min(rows_left, small_rows_per_batch);
-        if ((rc = pread_zero(dat.fd, hdata.p, B * small_row, processed))) return rc;
-        HEC_HIP(hipMemcpyAsync(ddata.p, hdata.p, B * small_row, hipMemcpyHostToDevice, s));
-        if ((rc = run_apply(gd->encode, K, ddata.p, small_row, small, dpar.p, small * M, small, small,
-                            uint32_t(B), nullptr, nullptr, s)))
-            return rc;
-        HEC_HIP(hipMemcpyAsync(hpar.p, dpar.p, B * small * M, hipMemcpyDeviceToHost, s));
-        HEC_HIP(hipStreamSynchronize(s));
-        for (uint64_t r = 0; r < B; ++r) {
-            for (int j = 0; j < K; ++j)
-                if ((rc = pwrite_all(out[j].fd, hdata.p + r * small_row + j * small, small, out_off + r * small)))
-                    return rc;
-            for (int j = 0; j < M; ++j)
-                if ((rc = pwrite_all(out[K + j].fd, hpar.p + (r * M + j) * small, small, out_off + r * small)))
-                    return rc;
-        }
-        out_off += B * small;
-        processed += B * small_row;
-        remaining -= int64_t(B * small_row);
+    if (remaining > 0 && small % buf_size != 0 && !pipe.errors().failed()) {
+        int frc = pipe.drain();
+        if (frc) return frc;
+        return fail(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
+                    "unexpected block size " + std::to_string(small) + ", buffer size " + std::to_string(buf_size));
     }
-    return HEC_OK;
+    while (remaining > 0 && !pipe.errors().failed()) {
+        const uint64_t rows_left = (uint64_t(remaining) + small_row - 1) / small_row;
+        const uint64_t b = std::min(rows_left, B);
+        Job job;
+        add_reads(job.reads, dat.fd, 0, b * small_row, processed, small, kIoThreads);
+        job.h2d.push_back({0, 0, b * small_row});
+        // parity device/host layout [4][b][small]: each parity file gets one contiguous piece
+        job.kernel = [=](uint8_t* d, hipStream_t s) {
+            return run_apply(*enc, K, d, small_row, small, d + data_cap, small, b * small, small, uint32_t(b),
+                             nullptr, nullptr, s);
+        };
+        job.d2h.push_back({data_cap, data_cap, b * small * M});
+        for (int j = 0; j < K; ++j) {
+            WriteSeg ws{out[j].fd, out_off, {}};
+            for (uint64_t r = 0; r < b; ++r) ws.pieces.push_back({r * small_row + j * small, small});
+            job.writes.push_back(std::move(ws));
+        }
+        for (int j = 0; j < M; ++j) job.writes.push_back({out[K + j].fd, out_off, {{data_cap + j * b * small, b * small}}});
+        pipe.submit(std::move(job));
+        out_off += b * small;
+        processed += b * small_row;
+        remaining -= int64_t(b * small_row);
+    }
+    return pipe.drain();
 }
 
 static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t* n_ids) {
@@ -199,12 +486,12 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
         if (::stat(name.c_str(), &st) == 0) {
             has[i] = true;
             in[i].fd = ::open(name.c_str(), O_RDONLY);
-            if (in[i].fd < 0) return io_fail("open " + name);
+            if (in[i].fd < 0) return fail(HEC_ERR_IO, "open " + name + ": " + std::strerror(errno));
         } else {
-            if (errno != ENOENT) return io_fail("stat " + name);
+            if (errno != ENOENT) return fail(HEC_ERR_IO, "stat " + name + ": " + std::strerror(errno));
             has[i] = false;
             out[i].fd = ::open(name.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-            if (out[i].fd < 0) return io_fail("open " + name);
+            if (out[i].fd < 0) return fail(HEC_ERR_IO, "open " + name + ": " + std::strerror(errno));
             rebuilt.push_back(uint32_t(i));
         }
     }
@@ -224,7 +511,7 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
         if (!has[i]) continue;
         ++npresent;
         struct stat st;
-        if (::fstat(in[i].fd, &st) != 0) return io_fail("stat shard");
+        if (::fstat(in[i].fd, &st) != 0) return fail(HEC_ERR_IO, std::string("stat shard: ") + std::strerror(errno));
         size[i] = uint64_t(st.st_size);
     }
     uint64_t row_size = 0;  // input_buffer_data_size
@@ -254,10 +541,6 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
             break;
         }
         ++rows;
-        if (npresent == N) {
-            // reconstruct is a no-op; the loop only re-checks sizes.
-            continue;
-        }
     }
 
     if (rows > 0 && npresent < N) {
@@ -269,42 +552,37 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
         if ((rc = decode_plan(rs.rs, present, false, coefs, in_ids, out_ids, &noop))) return rc;
         HostPlans hp;
         hp.add(coefs, in_ids, out_ids);
-        hipStream_t s;
-        HEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        struct StreamGuard {
-            hipStream_t s;
-            ~StreamGuard() { (void)hipStreamDestroy(s); }
-        } sg{s};
         DevicePlanSet ps;
         struct PsGuard {
             DevicePlanSet& p;
             ~PsGuard() { p.release(); }
         } pg{ps};
-        if ((rc = ps.upload(hp, nullptr, s))) return rc;
+        if ((rc = ps.upload(hp, nullptr, nullptr))) return rc;
         const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(rows, kBatchBytes / (K * row_size)));
-        const uint64_t slot = B * row_size;  // bytes per shard slot
-        Pinned host;
-        DevBuf dev;
-        HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&host.p), slot * N, hipHostMallocDefault));
-        HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dev.p), slot * N));
-        for (uint64_t r0 = 0; r0 < rows; r0 += B) {
+        const uint64_t slot = B * row_size;  // bytes per shard slot: layout [14][B rows]
+        PipelineLease lease;
+        if ((rc = lease_pipeline(slot * N, slot * N, lease))) return rc;
+        FilePipeline& pipe = *lease.pipe;
+        const DevicePlanSet* psp = &ps;
+        for (uint64_t r0 = 0; r0 < rows && !pipe.errors().failed(); r0 += B) {
             const uint64_t nr = std::min(B, rows - r0);
             const uint64_t off = r0 * row_size;
+            Job job;
             for (uint32_t id : in_ids) {
-                if ((rc = pread_zero(in[id].fd, host.p + id * slot, nr * row_size, off))) return rc;
-                HEC_HIP(hipMemcpyAsync(dev.p + id * slot, host.p + id * slot, nr * row_size,
-                                       hipMemcpyHostToDevice, s));
+                add_reads(job.reads, in[id].fd, id * slot, nr * row_size, off, row_size, 1);
+                job.h2d.push_back({id * slot, id * slot, nr * row_size});
             }
-            if ((rc = run_apply(ps, K, dev.p, row_size, slot, dev.p, row_size, slot, row_size, uint32_t(nr),
-                                nullptr, nullptr, s)))
-                return rc;
-            for (uint32_t id : out_ids)
-                HEC_HIP(hipMemcpyAsync(host.p + id * slot, dev.p + id * slot, nr * row_size,
-                                       hipMemcpyDeviceToHost, s));
-            HEC_HIP(hipStreamSynchronize(s));
-            for (uint32_t id : out_ids)
-                if ((rc = pwrite_all(out[id].fd, host.p + id * slot, nr * row_size, off))) return rc;
+            job.kernel = [=](uint8_t* d, hipStream_t s) {
+                return run_apply(*psp, K, d, row_size, slot, d, row_size, slot, row_size, uint32_t(nr), nullptr,
+                                 nullptr, s);
+            };
+            for (uint32_t id : out_ids) {
+                job.d2h.push_back({id * slot, id * slot, nr * row_size});
+                job.writes.push_back({out[id].fd, off, {{id * slot, nr * row_size}}});
+            }
+            pipe.submit(std::move(job));
         }
+        if ((rc = pipe.drain())) return rc;
     }
     if (end_rc != HEC_OK) return fail(end_rc, end_detail);
     if (n_ids) *n_ids = rebuilt.size();

@@ -46,6 +46,11 @@ def lib():
         L.orc_invert.argtypes = [P, P, ctypes.c_int]
         L.orc_invert.restype = ctypes.c_int
         L.orc_have_avx2.restype = ctypes.c_int
+        L.orc_write_ec_files.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_int]
+        L.orc_write_ec_files.restype = ctypes.c_int
+        L.orc_rebuild_ec_files.argtypes = [ctypes.c_char_p, P, P, ctypes.c_int]
+        L.orc_rebuild_ec_files.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -100,3 +105,18 @@ def splitmix64_bytes(seed: int, nbytes: int) -> np.ndarray:
     out = np.empty(nbytes, dtype=np.uint8)
     lib().orc_splitmix64_fill(seed, out.ctypes.data, nbytes)
     return out
+
+
+def write_ec_files(base: str, buf_size: int = 256 * 1024, large: int = 1 << 30, small: int = 1 << 20,
+                   simd: bool = True) -> int:
+    """C restatement of helyim_ec::write_ec_files (encoder.rs:39-242)."""
+    return lib().orc_write_ec_files(base.encode(), buf_size, large, small, int(simd))
+
+
+def rebuild_ec_files(base: str, simd: bool = True):
+    """C restatement of helyim_ec::rebuild_ec_files; -> (rc, rebuilt ids)."""
+    ids = (ctypes.c_uint32 * 14)()
+    n = ctypes.c_size_t(0)
+    rc = lib().orc_rebuild_ec_files(base.encode(), ctypes.cast(ids, ctypes.c_void_p),
+                                    ctypes.cast(ctypes.pointer(n), ctypes.c_void_p), int(simd))
+    return rc, [int(ids[i]) for i in range(n.value)]

@@ -246,3 +246,140 @@ void orc_splitmix64_fill(uint64_t seed, uint8_t* out, size_t nbytes) {
         }
     }
 }
+
+/* ---- file layer: restatement of helyim-ec/src/encoder.rs ------------------
+ * orc_write_ec_files  <- write_ec_files / generate_ec_files / encode_data_file
+ *                        (encoder.rs:39-46, 52-71, 129-242): rows of 10 blocks
+ *                        (large while remaining > 10*large, strict), 256 KiB
+ *                        batches, short reads zero-filled, 14 sequential writes.
+ * orc_rebuild_ec_files <- rebuild_ec_files / generate_missing_ec_files /
+ *                        rebuild_ec_files_inner (encoder.rs:48-50, 73-109, 244-307).
+ * Return 0, or: -1 io, -2 UnexpectedBlockSize, -3 UnexpectedEcShardSize,
+ * -4 TooFewShardsPresent. Single thread, like helyim. */
+#include <fcntl.h>
+#include <stdio.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+static int read_full(int fd, uint8_t* buf, size_t n, off_t off, size_t* got) {
+    size_t g = 0;
+    while (g < n) {
+        ssize_t r = pread(fd, buf + g, n - g, off + (off_t)g);
+        if (r < 0) return -1;
+        if (r == 0) break;
+        g += (size_t)r;
+    }
+    *got = g;
+    return 0;
+}
+
+static int write_full(int fd, const uint8_t* buf, size_t n) {
+    size_t p = 0;
+    while (p < n) {
+        ssize_t w = write(fd, buf + p, n - p);
+        if (w < 0) return -1;
+        p += (size_t)w;
+    }
+    return 0;
+}
+
+int orc_write_ec_files(const char* base, uint64_t buf_size, uint64_t large, uint64_t small, int simd) {
+    char name[4096];
+    snprintf(name, sizeof name, "%s.dat", base);
+    int dat = open(name, O_RDONLY);
+    if (dat < 0) return -1;
+    struct stat st;
+    if (fstat(dat, &st) != 0) { close(dat); return -1; }
+    int64_t remaining = (int64_t)st.st_size;
+    void* rs = orc_rs_new(10, 4);
+    uint8_t* bufs[14];
+    for (int i = 0; i < 14; i++) bufs[i] = (uint8_t*)malloc(buf_size);
+    int out[14];
+    for (int i = 0; i < 14; i++) {
+        snprintf(name, sizeof name, "%s.ec%02d", base, i);
+        out[i] = open(name, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    }
+    int rc = 0;
+    uint64_t processed = 0;
+    for (int phase = 0; phase < 2 && rc == 0; phase++) {
+        uint64_t block = phase == 0 ? large : small;
+        while (rc == 0 && (phase == 0 ? remaining > (int64_t)(large * 10) : remaining > 0)) {
+            if (block % buf_size != 0) { rc = -2; break; }
+            for (uint64_t b = 0; b < block / buf_size && rc == 0; b++) {
+                uint64_t start = processed + b * buf_size;
+                for (int i = 0; i < 10; i++) {
+                    size_t got = 0;
+                    if (read_full(dat, bufs[i], buf_size, (off_t)(start + block * i), &got)) { rc = -1; break; }
+                    if (got < buf_size) memset(bufs[i] + got, 0, buf_size - got);
+                }
+                if (rc) break;
+                orc_encode(rs, bufs, buf_size, simd);
+                for (int i = 0; i < 14; i++)
+                    if (write_full(out[i], bufs[i], buf_size)) { rc = -1; break; }
+            }
+            processed += block * 10;
+            remaining -= (int64_t)(block * 10);
+        }
+    }
+    for (int i = 0; i < 14; i++) { close(out[i]); free(bufs[i]); }
+    close(dat);
+    orc_rs_free(rs);
+    return rc;
+}
+
+int orc_rebuild_ec_files(const char* base, uint32_t* ids, size_t* n_ids, int simd) {
+    char name[4096];
+    int in[14], out[14];
+    uint8_t has[14];
+    size_t nr = 0;
+    for (int i = 0; i < 14; i++) {
+        snprintf(name, sizeof name, "%s.ec%02d", base, i);
+        struct stat st;
+        in[i] = out[i] = -1;
+        if (stat(name, &st) == 0) {
+            has[i] = 1;
+            in[i] = open(name, O_RDONLY);
+        } else {
+            has[i] = 0;
+            out[i] = open(name, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+            ids[nr++] = (uint32_t)i;
+        }
+    }
+    *n_ids = nr;
+    void* rs = orc_rs_new(10, 4);
+    const size_t SB = 1 << 20;
+    uint8_t* bufs[14];
+    for (int i = 0; i < 14; i++) bufs[i] = (uint8_t*)calloc(1, SB);
+    int rc = 0;
+    uint64_t start = 0;
+    size_t size = 0;
+    for (;;) {
+        int stop = 0;
+        for (int i = 0; i < 14 && !stop && rc == 0; i++) {
+            if (!has[i]) continue;
+            size_t got = 0;
+            if (read_full(in[i], bufs[i], SB, (off_t)start, &got)) { rc = -1; break; }
+            if (got == 0) { stop = 1; break; }
+            if (size == 0) size = got;
+            if (size != got) rc = -3;
+        }
+        if (stop || rc) break;
+        int npres = 0;
+        for (int i = 0; i < 14; i++) npres += has[i];
+        if (npres < 10) { rc = -4; break; }
+        if (npres < 14) {
+            orc_reconstruct(rs, bufs, has, SB, 0, simd);
+            for (int i = 0; i < 14; i++)
+                if (!has[i] && pwrite(out[i], bufs[i], size, (off_t)start) != (ssize_t)size) { rc = -1; break; }
+        }
+        if (rc) break;
+        start += size;
+    }
+    for (int i = 0; i < 14; i++) {
+        if (in[i] >= 0) close(in[i]);
+        if (out[i] >= 0) close(out[i]);
+        free(bufs[i]);
+    }
+    orc_rs_free(rs);
+    return rc;
+}

@@ -205,3 +205,30 @@ def test_volume_fixture(golden, tmp_path):
     vol = O.synthetic_volume(g["dat_bytes"])
     assert O.sha256(vol) == g["dat_sha256"]
     assert g["shard_bytes"] == [3 * (1 << 20)] * 14
+
+
+def test_c_oracle_file_layer_vs_fixture(golden, tmp_path):
+    g = golden("volume_30mb.json")
+    base = str(tmp_path / "1")
+    open(base + ".dat", "wb").write(O.synthetic_volume(g["dat_bytes"]).tobytes())
+    assert corc.write_ec_files(base) == 0
+    shas = [O.sha256(open(base + O.to_ext(i), "rb").read()) for i in range(14)]
+    assert shas == g["shard_sha256"]
+    for drop in g["drops"]:
+        for i in drop:
+            os.remove(base + O.to_ext(i))
+        rc, ids = corc.rebuild_ec_files(base)
+        assert rc == 0 and ids == sorted(drop)
+        assert [O.sha256(open(base + O.to_ext(i), "rb").read()) for i in range(14)] == g["shard_sha256"]
+
+
+@pytest.mark.parametrize("size", [1, 641, 6400 * 2 + 3])
+def test_c_oracle_file_layer_small_geometry(tmp_path, size):
+    dat = O.splitmix64_bytes(7 + size, size).tobytes()
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    for base in (a, b):
+        open(base + ".dat", "wb").write(dat)
+    assert corc.write_ec_files(a, 16, 640, 32) == 0
+    O.write_ec_files(b, 16, 640, 32)
+    for i in range(14):
+        assert open(a + O.to_ext(i), "rb").read() == open(b + O.to_ext(i), "rb").read()

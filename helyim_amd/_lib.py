@@ -58,6 +58,12 @@ SIGNATURES = {
     "hec_write_ec_files": (_I, [ctypes.c_char_p]),
     "hec_write_ec_files_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64]),
     "hec_rebuild_ec_files": (_I, [ctypes.c_char_p, ctypes.POINTER(_U32), ctypes.POINTER(_S)]),
+    "hec_write_sorted_file_from_index": (_I, [ctypes.c_char_p, ctypes.c_char_p]),
+    "hec_rebuild_ecx_file": (_I, [ctypes.c_char_p]),
+    "hec_save_volume_info": (_I, [ctypes.c_char_p, _U32]),
+    "hec_find_data_filesize": (_I, [ctypes.c_char_p, ctypes.POINTER(_U64)]),
+    "hec_write_data_file": (_I, [ctypes.c_char_p, ctypes.c_int64]),
+    "hec_write_index_file_from_ec_index": (_I, [ctypes.c_char_p]),
     "hec_set_launch_config": (_I, [_I, ctypes.c_long, _I, _I]),
     "hec_set_kernel_mode": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),

@@ -176,6 +176,24 @@ int hec_write_ec_files_ex(const char* base_filename, uint64_t buf_size, uint64_t
  * the rebuilt shard ids in ascending order, *n_rebuilt their count. */
 int hec_rebuild_ec_files(const char* base_filename, uint32_t* rebuilt_ids, size_t* n_rebuilt);
 
+/* ---- EC volume files around the shards (host-side byte formats) ----------- */
+/* write_sorted_file_from_index(base, ext) (encoder.rs:21-37): replay base.idx
+ * (16-byte BE entries; offset 0 or negative size deletes) and write the live
+ * entries sorted by needle id to base+ext (".ecx"). */
+int hec_write_sorted_file_from_index(const char* base_filename, const char* ext);
+/* rebuild_ecx_file(base) (lib.rs:95-133): apply base.ecj tombstones to base.ecx,
+ * then delete base.ecj; no .ecj -> HEC_OK. */
+int hec_rebuild_ecx_file(const char* base_filename);
+/* save_volume_info(filename, VolumeInfo{version}) as the generate RPC writes it
+ * (volume_info.rs:121-132, server.rs:470-475). */
+int hec_save_volume_info(const char* filename, uint32_t version);
+/* find_data_filesize(base) (decoder.rs:46-66). */
+int hec_find_data_filesize(const char* base_filename, uint64_t* data_filesize);
+/* write_data_file(base, size) (decoder.rs:142-180): .ec00-.ec09 -> base.dat. */
+int hec_write_data_file(const char* base_filename, int64_t data_filesize);
+/* write_index_file_from_ec_index(base) (decoder.rs:22-44): .ecx + .ecj -> .idx. */
+int hec_write_index_file_from_ec_index(const char* base_filename);
+
 /* ---- tuning / introspection ----------------------------------------------- */
 /* Kernel launch configuration (process-wide; speed only, results identical):
  * vec_per_thread 16-byte vectors per lane per chunk (1, 2, 4); max_blocks

@@ -425,3 +425,124 @@ def sha256(b) -> str:
     if isinstance(b, np.ndarray):
         b = b.tobytes()
     return hashlib.sha256(b).hexdigest()
+
+
+# --------------------------------------------------------------------------
+# EC volume files around the shards -- restated from the reference:
+#   .idx/.ecx entries: 16 bytes big endian (u64 needle id, u32 offset/8, i32 size)
+#   helyim-common/src/types/needle.rs:119-160, helyim-ec/src/needle/mod.rs:12-44
+# --------------------------------------------------------------------------
+import struct as _struct
+
+
+class IoError(Exception):
+    pass
+
+
+def _entries(raw: bytes):
+    return [_struct.unpack(">QIi", raw[i:i + 16]) for i in range(0, len(raw) - len(raw) % 16, 16)]
+
+
+def write_sorted_file_from_index(base: str, ext: str = ".ecx") -> None:
+    """encoder.rs:21-37 + SortedIndexMap::load_from_index (needle/mod.rs:12-32):
+    IndexMap insert / shift_remove replay, then ascending sort by key."""
+    with open(base + ".idx", "rb") as f:
+        raw = f.read()
+    live = {}
+    for key, off, size in _entries(raw):
+        if off == 0 or size < 0:          # Size::is_deleted: size < 0 || size == -1
+            live.pop(key, None)
+        else:
+            live[key] = (off, size)
+    if len(raw) % 16:                     # walk_index_file: read_exact of a partial entry
+        raise IoError("UnexpectedEof")
+    with open(base + ext, "wb") as f:
+        for key in sorted(live):
+            f.write(_struct.pack(">QIi", key, *live[key]))
+
+
+def rebuild_ecx_file(base: str) -> None:
+    """lib.rs:95-133 (binary search :54-82, tombstone write :88-93)."""
+    ecj = base + ".ecj"
+    if not os.path.exists(ecj):
+        return
+    with open(base + ".ecx", "r+b") as ecx:
+        raw = bytearray(ecx.read())
+        n = len(raw) // 16
+        ids = open(ecj, "rb").read()
+        for p in range(0, len(ids) - len(ids) % 8, 8):
+            want = _struct.unpack(">Q", ids[p:p + 8])[0]
+            lo, hi = 0, n
+            while lo < hi:
+                mid = (lo + hi) // 2
+                key = _struct.unpack(">Q", raw[mid * 16:mid * 16 + 8])[0]
+                if key == want:
+                    raw[mid * 16 + 12:mid * 16 + 16] = _struct.pack(">i", -1)
+                    break
+                if key < want:
+                    lo = mid + 1
+                else:
+                    hi = mid
+        ecx.seek(0)
+        ecx.write(raw)
+    os.remove(ecj)
+
+
+def volume_info_json(version: int) -> bytes:
+    """serde_json of VolumeInfo { version, ..Default } (volume.proto:75-79)."""
+    return ('{"files":[],"version":%d,"replication":""}' % version).encode()
+
+
+def find_data_filesize(base: str) -> int:
+    """decoder.rs:46-66 (Offset::actual_offset is a wrapping u32 product)."""
+    with open(base + ".ec00", "rb") as f:
+        sb = f.read(8)
+    if len(sb) < 8:
+        raise IoError("UnexpectedEof")
+    if sb[3] > 6:
+        raise IoError("Ttl error: invalid unit")
+    size = 0
+    for key, off, s in _entries(open(base + ".ecx", "rb").read()):
+        if s < 0:
+            continue
+        body = 16 + s + 4
+        stop = ((off * 8) & 0xFFFFFFFF) + body + (8 - body % 8)
+        size = max(size, stop)
+    return size
+
+
+def write_data_file(base: str, data_filesize: int) -> None:
+    """decoder.rs:142-180 (large rows while size >= 10 GiB, then 1 MiB blocks)."""
+    ins = [open(base + to_ext(i), "rb") for i in range(10)]
+    try:
+        with open(base + ".dat", "wb") as out:
+            L, S = ERASURE_CODING_LARGE_BLOCK_SIZE, ERASURE_CODING_SMALL_BLOCK_SIZE
+            while data_filesize >= 10 * L:
+                for f in ins:
+                    b = f.read(L)
+                    if len(b) < L:
+                        raise IoError("UnexpectedEof")
+                    out.write(b)
+                    data_filesize -= L
+            while data_filesize > 0:
+                for f in ins:
+                    n = min(data_filesize, S)
+                    b = f.read(n)
+                    if len(b) < n:
+                        raise IoError("UnexpectedEof")
+                    out.write(b)
+                    data_filesize -= n
+    finally:
+        for f in ins:
+            f.close()
+
+
+def write_index_file_from_ec_index(base: str) -> None:
+    """decoder.rs:22-44: .ecx copied, then a deleted entry per .ecj id."""
+    raw = open(base + ".ecx", "rb").read()
+    with open(base + ".idx", "wb") as out:
+        out.write(raw)
+        if os.path.exists(base + ".ecj"):
+            ids = open(base + ".ecj", "rb").read()
+            for p in range(0, len(ids) - len(ids) % 8, 8):
+                out.write(ids[p:p + 8] + _struct.pack(">Ii", 0, -1))

@@ -50,6 +50,7 @@ SIGNATURES = {
     "hec_rs_verify": (_I, [_P, _P, _P, _S, ctypes.POINTER(_I)]),
     "hec_rs_reconstruct": (_I, [_P, _P, _P, _P, _S]),
     "hec_rs_reconstruct_data": (_I, [_P, _P, _P, _P, _S]),
+    "hec_rs_reconstruct_batch": (_I, [_P, _P, _P, _P, _S, _I, ctypes.POINTER(_S)]),
     "hec_gpu_encode_batch": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32, _P]),
     "hec_gpu_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P]),
     "hec_host_encode_batch": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32]),

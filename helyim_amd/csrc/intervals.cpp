@@ -1,0 +1,209 @@
+// Batched reconstruct of many small, independent stripes in one launch: the
+// degraded-read path (helyim-store/src/erasure_coding/mod.rs:403-491 calls
+// ReedSolomon::reconstruct once per needle interval, bytes to KiB each).
+// Stripes are packed back to back into one pinned staging area, copied to the
+// GPU once, decoded by rs104_ragged_kernel (one workgroup per 4 KiB chunk of
+// each stripe, per-stripe length and erasure pattern), and copied back once.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <thread>
+
+#include "hec_internal.hpp"
+
+namespace hec {
+namespace {
+
+struct RaggedScratch {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    uint8_t* hmeta = nullptr;
+    uint8_t* dmeta = nullptr;
+    size_t mcap = 0;
+    int reserve(size_t bytes, size_t meta) {
+        if (!stream) HEC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        if (bytes > cap) {
+            if (host) HEC_HIP(hipHostFree(host));
+            if (dev) HEC_HIP(hipFree(dev));
+            host = dev = nullptr;
+            cap = 0;
+            const size_t want = std::max(bytes, size_t(64) << 20);
+            HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), want, hipHostMallocDefault));
+            HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dev), want));
+            cap = want;
+        }
+        if (meta > mcap) {
+            if (hmeta) HEC_HIP(hipHostFree(hmeta));
+            if (dmeta) HEC_HIP(hipFree(dmeta));
+            hmeta = dmeta = nullptr;
+            mcap = 0;
+            const size_t want = std::max(meta, size_t(1) << 20);
+            HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&hmeta), want, hipHostMallocDefault));
+            HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dmeta), want));
+            mcap = want;
+        }
+        return HEC_OK;
+    }
+};
+
+int ragged_scratch(RaggedScratch** out) {
+    static std::mutex mu;
+    static std::map<int, RaggedScratch*>* reg = new std::map<int, RaggedScratch*>();  // process lifetime
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& p = (*reg)[dev];
+    if (!p) p = new RaggedScratch();
+    *out = p;
+    return HEC_OK;
+}
+
+// Run fn(i) for i in [0, n) on up to 16 threads (host memcpy of the packing).
+template <typename F>
+void parallel_for(size_t n, uint64_t bytes, F fn) {
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = unsigned(std::min<uint64_t>(hw, std::max<uint64_t>(1, bytes >> 22)));  // >= 4 MiB/thread
+    if (nt <= 1 || n < 2) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = t; i < n; i += nt) fn(i);
+        });
+    for (auto& x : th) x.join();
+}
+
+}  // namespace
+}  // namespace hec
+
+using namespace hec;
+
+extern "C" {
+
+int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const size_t* lens, const uint8_t* present,
+                             size_t n_stripes, int data_only, size_t* bad_index) {
+    if (!rs || (n_stripes && (!shards || !lens || !present))) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    const int k = rs->k, n = rs->n;
+    if (bad_index) *bad_index = n_stripes;
+    // 1. validate every stripe first (upstream reconstruct checks, per stripe)
+    struct Active {
+        size_t s;
+        uint64_t L, Lp, off, out_off;
+        uint32_t mask;
+    };
+    std::vector<Active> act;
+    uint64_t total = 0;
+    for (size_t s = 0; s < n_stripes; ++s) {
+        const uint8_t* pr = present + s * n;
+        uint64_t L = 0;
+        int np = 0, err = HEC_OK;
+        uint32_t mask = 0;
+        for (int i = 0; i < n && !err; ++i) {
+            if (!pr[i]) continue;
+            const size_t li = lens[s * n + i];
+            if (li == 0) err = HEC_ERR_EMPTY_SHARD;
+            else if (np && li != L) err = HEC_ERR_INCORRECT_SHARD_SIZE;
+            L = li;
+            ++np;
+            mask |= 1u << i;
+        }
+        if (!err && np < n && np < k) err = HEC_ERR_TOO_FEW_SHARDS_PRESENT;
+        if (!err && np < n)
+            for (int i = 0; i < n; ++i)
+                if (!pr[i] && !(data_only && i >= k) && !shards[s * n + i])
+                    err = fail(HEC_ERR_INVALID_ARGUMENT, "missing shard without a buffer");
+        if (err) {
+            if (bad_index) *bad_index = s;
+            return err;
+        }
+        if (np == n) continue;  // upstream no-op
+        const uint64_t Lp = (L + 15) / 16 * 16;
+        act.push_back({s, L, Lp, total, 0, mask});
+        total += (uint64_t(k) * Lp + 255) / 256 * 256;  // compact inputs: the first k present shards
+    }
+    if (act.empty()) return HEC_OK;
+    const uint64_t in_total = total;
+    for (Active& a : act) {  // compact outputs: the erased shards, ascending
+        a.out_off = total;
+        total += (uint64_t(n - __builtin_popcount(a.mask)) * a.Lp + 255) / 256 * 256;
+    }
+
+    // Other geometries: one host-API reconstruct per stripe (same kernels, generic path).
+    if (!(k == 10 && rs->m == 4)) {
+        for (const Active& a : act) {
+            int rc = data_only ? hec_rs_reconstruct_data(rs, shards + a.s * n, lens + a.s * n, present + a.s * n, n)
+                               : hec_rs_reconstruct(rs, shards + a.s * n, lens + a.s * n, present + a.s * n, n);
+            if (rc) {
+                if (bad_index) *bad_index = a.s;
+                return rc;
+            }
+        }
+        return HEC_OK;
+    }
+
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    RaggedScratch* sc;
+    if ((rc = ragged_scratch(&sc))) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    std::vector<RaggedItem> items(act.size());
+    std::vector<uint32_t> block_item;
+    for (size_t j = 0; j < act.size(); ++j) {
+        const Active& a = act[j];
+        const uint32_t chunks = uint32_t((a.L + 4095) / 4096);
+        items[j] = RaggedItem{a.off, a.Lp, uint32_t(a.L), a.mask, uint32_t(block_item.size()), 0, a.out_off};
+        block_item.insert(block_item.end(), chunks, uint32_t(j));
+    }
+    const size_t items_bytes = items.size() * sizeof(RaggedItem);
+    const size_t meta = (items_bytes + 255) / 256 * 256 + block_item.size() * 4;
+    if ((rc = sc->reserve(total, meta))) return rc;
+    if ((rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
+    // 2. pack the survivors the decode reads (first k present shards) into slots 0..k-1
+    parallel_for(act.size(), in_total, [&](size_t j) {
+        const Active& a = act[j];
+        int used = 0;
+        for (int i = 0; i < n && used < k; ++i)
+            if ((a.mask >> i) & 1) {
+                std::memcpy(sc->host + a.off + used * a.Lp, shards[a.s * n + i], a.L);
+                ++used;
+            }
+    });
+    std::memcpy(sc->hmeta, items.data(), items_bytes);
+    const size_t map_off = (items_bytes + 255) / 256 * 256;
+    std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
+    HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, sc->stream));
+    HEC_HIP(hipMemcpyAsync(sc->dev, sc->host, in_total, hipMemcpyHostToDevice, sc->stream));
+    RaggedArgs ra{};
+    ra.base = sc->dev;
+    ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
+    ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
+    ra.n_blocks = uint32_t(block_item.size());
+    ra.tabs = gd->decode_dense.tabs;
+    ra.lut = gd->decode_dense.lut;
+    ra.compact = 1;
+    HEC_HIP(launch_rs104_ragged(ra, true, sc->stream));
+    HEC_HIP(hipMemcpyAsync(sc->host + in_total, sc->dev + in_total, total - in_total, hipMemcpyDeviceToHost,
+                           sc->stream));
+    HEC_HIP(hipStreamSynchronize(sc->stream));
+    // 3. hand back the erased shards (data shards only for reconstruct_data)
+    parallel_for(act.size(), total - in_total, [&](size_t j) {
+        const Active& a = act[j];
+        int r = 0;
+        for (int i = 0; i < n; ++i)
+            if (!((a.mask >> i) & 1)) {
+                if (!(data_only && i >= k)) std::memcpy(shards[a.s * n + i], sc->host + a.out_off + r * a.Lp, a.L);
+                ++r;
+            }
+    });
+    return HEC_OK;
+}
+
+}  // extern "C"

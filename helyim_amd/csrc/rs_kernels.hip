@@ -233,20 +233,21 @@ __device__ __forceinline__ uint32_t remap_block(uint32_t b, uint32_t nb, uint32_
     return (j / mode) * (8 * mode) + x * mode + (j % mode);
 }
 
-template <bool DEC, bool XORONLY>
-__global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
+// One 4 KiB chunk of one RS(10,4) stripe. Encode (DEC=false): inputs 0..9 at
+// in_b, outputs 0..3 at out_b. Decode (DEC=true): in place at in_b == out_b,
+// shard ids from the present mask, tables at lut[mask] * 200 words.
+template <bool DEC, bool XORONLY, bool COMPACT = false>
+__device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
+                                            uint64_t out_shard, uint64_t len, uint32_t chunk, uint32_t mask_in,
+                                            cu32p tab, cu32p lut, uint32_t* bad_count) {
     constexpr int K = 10, N = 14, R = 4;
-    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap);
-    const uint32_t stripe = item / a.chunks_per_stripe;
-    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
     uint32_t in_id[K], out_id[R];
     uint32_t nout = R;
-    cu32p tab = as_const(a.tabs);
     if constexpr (DEC) {
-        const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
+        const uint32_t mask = mask_in & ((1u << N) - 1);
         const uint32_t present = __builtin_popcount(mask);
         if (present < K) {
-            if (chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
+            if (chunk == 0 && threadIdx.x == 0 && bad_count) atomicAdd(bad_count, 1u);
             return;
         }
         if (present == N) return;  // upstream: all present -> no-op
@@ -254,34 +255,32 @@ __global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
         uint32_t m = mask;
 #pragma unroll
         for (int i = 0; i < K; ++i) {  // first K present shards, ascending
-            in_id[i] = __builtin_ctz(m);
+            in_id[i] = COMPACT ? i : __builtin_ctz(m);
             m &= m - 1;
         }
         uint32_t e = ~mask & ((1u << N) - 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {  // erased shards, ascending
-            out_id[r] = e ? __builtin_ctz(e) : 0;
+            out_id[r] = COMPACT ? r : (e ? __builtin_ctz(e) : 0);
             e &= e - 1;
         }
-        tab += as_const(a.lut)[mask] * (K * R * 5);
+        tab += lut[mask] * (K * R * 5);
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) in_id[i] = i;
 #pragma unroll
         for (int r = 0; r < R; ++r) out_id[r] = r;
     }
-    const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
-    uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
     const uint64_t o = uint64_t(chunk) * (kThreads * kVecBytes) + threadIdx.x * kVecBytes;
-    if (o >= a.len) return;
-    const uint64_t avail = a.len - o;
+    if (o >= len) return;
+    const uint64_t avail = len - o;
     u32x4 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
     if (avail >= kVecBytes) {
         u32x4 d[K];
 #pragma unroll
-        for (int i = 0; i < K; ++i) d[i] = load_full(in_b + uint64_t(in_id[i]) * a.in_shard + o, true);
+        for (int i = 0; i < K; ++i) d[i] = load_full(in_b + uint64_t(in_id[i]) * in_shard + o, true);
 #pragma unroll
         for (int i = 0; i < K; ++i) mac<R, XORONLY>(acc, d[i], tab + i * (R * 5));
         // Materialise every row before the uniform `r < nout` store branches:
@@ -291,15 +290,52 @@ __global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
         for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if (r < int(nout)) store_full(out_b + uint64_t(out_id[r]) * a.out_shard + o, acc[r], true);
+            if (r < int(nout)) store_full(out_b + uint64_t(out_id[r]) * out_shard + o, acc[r], true);
     } else {
         for (int i = 0; i < K; ++i) {
-            const u32x4 d = load_tail(in_b + uint64_t(in_id[i]) * a.in_shard + o, avail);
+            const u32x4 d = load_tail(in_b + uint64_t(in_id[i]) * in_shard + o, avail);
             gf_mac<R>(acc, d, tab + i * (R * 5));
         }
         for (int r = 0; r < R; ++r)
-            if (r < int(nout)) store_tail(out_b + uint64_t(out_id[r]) * a.out_shard + o, acc[r], avail);
+            if (r < int(nout)) store_tail(out_b + uint64_t(out_id[r]) * out_shard + o, acc[r], avail);
     }
+}
+
+template <bool DEC, bool XORONLY>
+__global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
+    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap);
+    const uint32_t stripe = item / a.chunks_per_stripe;
+    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
+    const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
+    rs104_chunk<DEC, XORONLY>(a.in_base + uint64_t(stripe) * a.in_stripe, a.out_base + uint64_t(stripe) * a.out_stripe,
+                              a.in_shard, a.out_shard, a.len, chunk, mask, as_const(a.tabs), as_const(a.lut),
+                              a.bad_count);
+}
+
+// Ragged batches: every stripe has its own length, shard stride and mask
+// (degraded reads of needle intervals, mixed 64 KiB-4 MiB stripes). The host
+// lays stripes out back to back and passes a workgroup -> stripe map.
+template <bool DEC, bool COMPACT>
+__global__ __launch_bounds__(kThreads) void rs104_ragged_kernel(RaggedArgs a) {
+    const uint32_t s = as_const(a.block_item)[blockIdx.x];
+    const __attribute__((address_space(4))) RaggedItem* it = as_const(a.items) + s;
+    const uint64_t off = it->off, stride = it->shard_stride;
+    const uint32_t len = it->len, mask = it->mask, first = it->first_block;
+    uint8_t* b = a.base + off;
+    uint8_t* o = COMPACT ? a.base + it->out_off : (DEC ? b : b + 10 * stride);
+    rs104_chunk<DEC, false, COMPACT>(b, o, stride, stride, len, blockIdx.x - first, mask, as_const(a.tabs),
+                                     as_const(a.lut), a.bad_count);
+}
+
+hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream) {
+    if (a.n_blocks == 0) return hipSuccess;
+    if (decode && a.compact)
+        hipLaunchKernelGGL((rs104_ragged_kernel<true, true>), dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
+    else if (decode)
+        hipLaunchKernelGGL((rs104_ragged_kernel<true, false>), dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
+    else
+        hipLaunchKernelGGL((rs104_ragged_kernel<false, false>), dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
 }
 
 template <bool DEC, bool XORONLY>

@@ -45,6 +45,33 @@ struct ApplyArgs {
                                  //    offset 0, decode = tables at lut[mask] * 200 words
 };
 
+// Ragged RS(10,4) batch (every stripe its own length / stride / mask); all
+// strides 16-byte aligned. Stripe s has shards at base + off + i*shard_stride
+// and owns workgroups [first_block, first_block + ceil(len / 4 KiB)).
+struct RaggedItem {
+    uint64_t off;          // shard 0 (full layout) or input slot 0 (compact layout)
+    uint64_t shard_stride;
+    uint32_t len;
+    uint32_t mask;         // present mask (decode); ignored by encode
+    uint32_t first_block;
+    uint32_t pad;
+    uint64_t out_off;      // compact decode: output slot 0 (erased shards, ascending)
+};
+
+struct RaggedArgs {
+    uint8_t* base;
+    const RaggedItem* items;
+    const uint32_t* block_item;  // workgroup -> stripe index
+    uint32_t n_blocks;
+    const uint32_t* tabs;        // encode plan tables, or the dense decode set
+    const uint32_t* lut;         // decode: mask -> plan id
+    uint32_t* bad_count;
+    uint32_t compact;            // decode: inputs = slots 0..9 at off (the first 10 present
+                                 // shards), outputs = slots 0..e-1 at out_off (erased shards)
+};
+
+hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream);
+
 struct LaunchConfig {
     int vec_per_thread = 1;      // 16-byte vectors per lane per chunk (1, 2 or 4)
     long max_blocks = 0;         // grid cap (0 = one block per chunk)

@@ -113,3 +113,44 @@ class ReedSolomon:
         check(rc(self._h, _ptr_array(arrs), _len_array(arrs), present, len(arrs)))
         for i in new:
             shards[i] = arrs[i]
+
+    def reconstruct_batch(self, stripes: Sequence[MutableSequence[Optional[object]]],
+                          data_only: bool = False) -> None:
+        """reconstruct() over many independent stripes (any lengths) in one GPU
+        round trip -- the batched form of the degraded-read reconstruct.
+        Raises the first failing stripe's error (attribute .stripe) with
+        nothing written."""
+        n = self.total_shard_count()
+        flat: List[Optional[np.ndarray]] = []
+        new = []
+        for si, shards in enumerate(stripes):
+            arrs = [None if s is None else _as_u8(s) for s in shards]
+            if len(arrs) != n:
+                from .errors import TooFewShards, TooManyShards
+                err = TooFewShards() if len(arrs) < n else TooManyShards()
+                err.stripe = si
+                raise err
+            lens = [a.size for a in arrs if a is not None]
+            L = lens[0] if lens else 0
+            if L and all(x == L for x in lens) and self._k <= len(lens) < n:
+                for i, a in enumerate(arrs):
+                    if a is None and not (data_only and i >= self._k):
+                        arrs[i] = np.zeros(L, dtype=np.uint8)
+                        new.append((si, i, arrs[i]))
+            flat.extend(arrs)
+        present = (ctypes.c_uint8 * len(flat))(*[0 if a is None else 1 for a in flat])
+        for si, shards in enumerate(stripes):  # presence comes from the caller's None slots
+            for i, s in enumerate(shards):
+                present[si * n + i] = 0 if s is None else 1
+        bad = ctypes.c_size_t(0)
+        rc = lib.hec_rs_reconstruct_batch(self._h, _ptr_array(flat), _len_array(
+            [None if (s is None) else a for s, a in zip([x for st in stripes for x in st], flat)]),
+            present, len(stripes), int(data_only), ctypes.byref(bad))
+        if rc:
+            try:
+                check(rc)
+            except Exception as e:
+                e.stripe = int(bad.value)
+                raise
+        for si, i, a in new:
+            stripes[si][i] = a

@@ -114,6 +114,17 @@ int hec_rs_reconstruct(const hec_rs_t* rs, uint8_t* const* shards, const size_t*
 int hec_rs_reconstruct_data(const hec_rs_t* rs, uint8_t* const* shards, const size_t* shard_lens,
                             const uint8_t* present, size_t n_shards);
 
+/* Batched ReedSolomon::reconstruct over n_stripes independent stripes of any
+ * lengths in ONE GPU round trip -- the degraded-read path
+ * (helyim-store/src/erasure_coding/mod.rs:403-491 reconstructs one needle
+ * interval per call). shards / lens / present are n_stripes * total entries,
+ * stripe-major; per stripe the semantics and errors are hec_rs_reconstruct's
+ * (reconstruct_data when data_only != 0). Every stripe is validated before
+ * any work; on error nothing is written and *bad_index (optional) names the
+ * first failing stripe. */
+int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const size_t* lens,
+                             const uint8_t* present, size_t n_stripes, int data_only, size_t* bad_index);
+
 /* ---- device-resident batches (no reference counterpart: the GPU form of the
  * encode_data_one_batch loop, encoder.rs:158-198, over many stripes) -------
  * Shard (stripe s, shard i) lives at base + s*stripe_stride + i*shard_stride.

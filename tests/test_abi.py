@@ -107,3 +107,17 @@ def test_file_layer_io_errors(tmp_path):
     import helyim_amd as H
     with pytest.raises(H.Io):
         H.write_ec_files(str(tmp_path / "missing"))
+
+
+def test_reconstruct_batch_validation_before_device():
+    import helyim_amd as H
+    rs = H.ReedSolomon(10, 4)
+    good = [np.zeros(8, np.uint8) for _ in range(14)]
+    rs.reconstruct_batch([list(good), list(good)])  # all present: no-op, no device work
+    bad = [None] * 5 + [np.zeros(8, np.uint8) for _ in range(9)]
+    with pytest.raises(H.TooFewShardsPresent) as ei:
+        rs.reconstruct_batch([list(good), bad])
+    assert ei.value.stripe == 1
+    with pytest.raises(H.IncorrectShardSize) as ei:
+        rs.reconstruct_batch([[None] + good[1:13] + [np.zeros(9, np.uint8)]])
+    assert ei.value.stripe == 0

@@ -229,7 +229,9 @@ def main():
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; more ranks than visible GPUs (a rehearsal on a
+    # one-GPU box) share devices round-robin
+    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
 
     import helyim_amd as H
     import helyim_amd.batch as B

@@ -67,6 +67,7 @@ SIGNATURES = {
     "hec_write_index_file_from_ec_index": (_I, [ctypes.c_char_p]),
     "hec_set_launch_config": (_I, [_I, ctypes.c_long, _I, _I]),
     "hec_set_kernel_mode": (_I, [_I]),
+    "hec_set_xcd_parts": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
 }
 

@@ -422,6 +422,12 @@ int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, in
     return HEC_OK;
 }
 
+int hec_set_xcd_parts(int parts) {
+    if (parts < 1 || parts > 1024) return fail(HEC_ERR_INVALID_ARGUMENT, "parts in 1..1024");
+    launch_config().xcd_parts = parts;
+    return HEC_OK;
+}
+
 int hec_set_kernel_mode(int mode) {
     if (mode != 0 && mode != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "mode must be 0 or 1");
     launch_config().mode = mode;

@@ -221,9 +221,15 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
 //   mode G >= 2: XCD x takes runs of G consecutive chunks, XCDs interleaved
 //               run by run (applied to the largest prefix divisible by 8G).
 // Always a bijection; speed only, never correctness.
-__device__ __forceinline__ uint32_t remap_block(uint32_t b, uint32_t nb, uint32_t mode) {
+__device__ __forceinline__ uint32_t remap_block(uint32_t b, uint32_t nb, uint32_t mode, uint32_t parts = 1) {
     if (mode == 0) return b;
     const uint32_t x = b % 8, j = b / 8;
+    if (mode == 1 && parts > 1 && nb % (8 * parts) == 0) {
+        // XCD x spreads its workgroups over `parts` regions of the batch:
+        // region x*parts + j%parts, position j/parts within it.
+        const uint32_t q = nb / (8 * parts);
+        return (x * parts + j % parts) * q + j / parts;
+    }
     if (mode == 1) {
         const uint32_t q = nb / 8, r = nb % 8;
         return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
@@ -303,7 +309,7 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
 
 template <bool DEC, bool XORONLY>
 __global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
-    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap);
+    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
     const uint32_t stripe = item / a.chunks_per_stripe;
     const uint32_t chunk = item - stripe * a.chunks_per_stripe;
     const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
@@ -345,6 +351,7 @@ static hipError_t launch_rs104(ApplyArgs a, const LaunchConfig& cfg, hipStream_t
     a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
+    a.xcd_parts = uint32_t(cfg.xcd_parts);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
     hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY>), dim3(uint32_t(a.n_items)), dim3(kThreads), lds, stream, a);
     return hipGetLastError();

@@ -213,6 +213,9 @@ int hec_write_index_file_from_ec_index(const char* base_filename);
  * of G consecutive chunks per XCD; blocks_per_cu > 0 caps resident
  * workgroups per CU (0 = no cap). */
 int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, int blocks_per_cu);
+/* With xcd_remap 1: the workgroups of one XCD work on `parts` regions of the
+ * batch concurrently (1 = one contiguous eighth per XCD). Speed only. */
+int hec_set_xcd_parts(int parts);
 /* Diagnostic: 0 = GF(2^8) coding (default); 1 = XOR-only bandwidth ceiling --
  * the RS(10,4) aligned kernel with its GF math replaced by plain XOR (same
  * loads, stores and addressing; WRONG parity by design), used only to measure

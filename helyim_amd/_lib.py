@@ -55,6 +55,8 @@ SIGNATURES = {
     "hec_gpu_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P]),
     "hec_host_encode_batch": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32]),
     "hec_host_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P]),
+    "hec_gpu_encode_ragged": (_I, [_P, _P, _P, _U32, _P]),
+    "hec_gpu_reconstruct_ragged": (_I, [_P, _P, _P, _U32, _P, _P]),
     "hec_gpu_fill_splitmix": (_I, [_P, _U64, _U64, _U32, _U64, _P]),
     "hec_write_ec_files": (_I, [ctypes.c_char_p]),
     "hec_write_ec_files_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64]),

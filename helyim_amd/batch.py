@@ -92,6 +92,30 @@ def host_reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks
     return int(bad.value)
 
 
+def _desc_array(descs):
+    """descs: iterable of (offset, shard_stride, shard_len, present_mask)."""
+    import numpy as np
+    dt = np.dtype([("offset", "<u8"), ("shard_stride", "<u8"), ("shard_len", "<u4"), ("present_mask", "<u4")])
+    return np.array([tuple(int(x) for x in d) for d in descs], dtype=dt)
+
+
+def encode_ragged(rs: ReedSolomon, base: torch.Tensor, descs, stream=None) -> None:
+    """RS(10,4) encode of stripes of mixed lengths in one launch; descs rows are
+    (byte offset of shard 0 in base, shard stride, shard length, unused)."""
+    d = _desc_array(descs)
+    check(lib.hec_gpu_encode_ragged(rs.handle, base.data_ptr(), d.ctypes.data, len(d), _stream_ptr(stream)))
+
+
+def reconstruct_ragged(rs: ReedSolomon, base: torch.Tensor, descs, bad_stripes: torch.Tensor = None,
+                       stream=None) -> None:
+    """Reconstruct stripes of mixed lengths and patterns in place, one launch;
+    descs rows are (offset, shard stride, shard length, present mask)."""
+    d = _desc_array(descs)
+    bad = bad_stripes.data_ptr() if bad_stripes is not None else None
+    check(lib.hec_gpu_reconstruct_ragged(rs.handle, base.data_ptr(), d.ctypes.data, len(d), bad,
+                                         _stream_ptr(stream)))
+
+
 def fill_splitmix(t: torch.Tensor, bytes_per_stripe: int, seed_base: int, stream=None) -> None:
     """Fill the first bytes_per_stripe bytes of each t[s] with splitmix64(seed_base + s)."""
     S = t.shape[0]

@@ -18,6 +18,7 @@ namespace {
 struct RaggedScratch {
     std::mutex mu;
     hipStream_t stream = nullptr;
+    hipEvent_t meta_free = nullptr;  // device-API calls: meta buffers reusable once this fires
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
     size_t cap = 0;
@@ -26,7 +27,7 @@ struct RaggedScratch {
     size_t mcap = 0;
     int reserve(size_t bytes, size_t meta) {
         if (!stream) HEC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        if (bytes > cap) {
+        if (bytes > cap && bytes > 0) {
             if (host) HEC_HIP(hipHostFree(host));
             if (dev) HEC_HIP(hipFree(dev));
             host = dev = nullptr;
@@ -204,6 +205,79 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
             }
     });
     return HEC_OK;
+}
+
+}  // extern "C"
+
+namespace hec {
+namespace {
+
+// Device-resident ragged batches: stripe descriptors come from the host, data
+// stays in HBM. Descriptors -> RaggedItems + workgroup map in pinned staging,
+// uploaded on the caller's stream ahead of the kernel.
+int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs, uint32_t n, bool decode,
+               uint32_t* d_bad, hipStream_t stream) {
+    if (!rs || !d_base || (n && !descs)) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (!(rs->k == 10 && rs->m == 4))
+        return fail(HEC_ERR_INVALID_ARGUMENT, "ragged device batches are RS(10,4) only");
+    std::vector<RaggedItem> items;
+    std::vector<uint32_t> block_item;
+    items.reserve(n);
+    for (uint32_t j = 0; j < n; ++j) {
+        const hec_stripe_desc& d = descs[j];
+        if (d.shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "stripe " + std::to_string(j));
+        if ((d.offset | d.shard_stride | uint64_t(reinterpret_cast<uintptr_t>(d_base))) % 16 != 0 ||
+            d.shard_stride < d.shard_len)
+            return fail(HEC_ERR_INVALID_ARGUMENT, "stripe " + std::to_string(j) +
+                                                      ": offset/stride must be 16-byte aligned, stride >= len");
+        const uint32_t chunks = (d.shard_len + 4095) / 4096;
+        items.push_back(RaggedItem{d.offset, d.shard_stride, d.shard_len, d.present_mask,
+                                   uint32_t(block_item.size()), 0, 0});
+        block_item.insert(block_item.end(), chunks, j);
+    }
+    if (items.empty()) return HEC_OK;
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    RaggedScratch* sc;
+    if ((rc = ragged_scratch(&sc))) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    const size_t items_bytes = items.size() * sizeof(RaggedItem);
+    const size_t map_off = (items_bytes + 255) / 256 * 256;
+    const size_t meta = map_off + block_item.size() * 4;
+    if (sc->meta_free) HEC_HIP(hipEventSynchronize(sc->meta_free));  // previous call's kernel done
+    if ((rc = sc->reserve(0, meta))) return rc;
+    if (!sc->meta_free) HEC_HIP(hipEventCreateWithFlags(&sc->meta_free, hipEventDisableTiming));
+    if (decode && (rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
+    std::memcpy(sc->hmeta, items.data(), items_bytes);
+    std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
+    HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, stream));
+    RaggedArgs ra{};
+    ra.base = d_base;
+    ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
+    ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
+    ra.n_blocks = uint32_t(block_item.size());
+    ra.tabs = decode ? gd->decode_dense.tabs : gd->encode.tabs;
+    ra.lut = decode ? gd->decode_dense.lut : nullptr;
+    ra.bad_count = d_bad;
+    HEC_HIP(launch_rs104_ragged(ra, decode, stream));
+    HEC_HIP(hipEventRecord(sc->meta_free, stream));
+    return HEC_OK;
+}
+
+}  // namespace
+}  // namespace hec
+
+extern "C" {
+
+int hec_gpu_encode_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs, uint32_t n_stripes,
+                          void* stream) {
+    return hec::gpu_ragged(rs, d_base, descs, n_stripes, false, nullptr, static_cast<hipStream_t>(stream));
+}
+
+int hec_gpu_reconstruct_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs,
+                               uint32_t n_stripes, uint32_t* d_bad_stripes, void* stream) {
+    return hec::gpu_ragged(rs, d_base, descs, n_stripes, true, d_bad_stripes, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

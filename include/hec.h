@@ -167,6 +167,24 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
                                uint64_t shard_stride, uint64_t shard_len, uint32_t n_stripes,
                                const uint32_t* h_present_masks, uint32_t* n_bad_stripes);
 
+/* Ragged device batches (RS(10,4)): every stripe has its own length, shard
+ * stride and erasure pattern -- BASELINE config 5's mixed 64 KiB-4 MiB
+ * stripes in ONE launch. Stripe j's shard i is at d_base + offset + i *
+ * shard_stride (offset, stride and d_base 16-byte aligned, stride >=
+ * shard_len). Encode reads shards 0..9 and writes 10..13; reconstruct uses
+ * present_mask like hec_gpu_reconstruct_batch. descs are HOST memory; the
+ * launch is asynchronous on `stream`. */
+typedef struct hec_stripe_desc {
+    uint64_t offset;
+    uint64_t shard_stride;
+    uint32_t shard_len;
+    uint32_t present_mask;
+} hec_stripe_desc;
+int hec_gpu_encode_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs,
+                          uint32_t n_stripes, void* stream);
+int hec_gpu_reconstruct_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs,
+                               uint32_t n_stripes, uint32_t* d_bad_stripes, void* stream);
+
 /* Deterministic splitmix64 stripe data (bench / test inputs): stripe s gets
  * bytes_per_stripe bytes at d_base + s*stripe_stride, 64-bit word n (n >= 1)
  * = splitmix64_mix(seed_base + s + n * 0x9E3779B97F4A7C15), little endian. */

@@ -243,3 +243,50 @@ def test_full_config_roundtrip(gpu):
     torch.cuda.synchronize()
     assert torch.equal(t[er], snap)
     assert t[:, 10:].view(torch.int64).sum(dtype=torch.int64).item() == parity_sum
+
+
+def test_ragged_device_batch(gpu):
+    """Mixed-length stripes (config 5 shape plus odd lengths) in one launch each
+    for encode and reconstruct, against the C oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    rng = np.random.default_rng(21)
+    lens = [1, 17, 1000, 4096, 4097, 65536, 100003, 1 << 20, 3 << 20] + \
+        [int(64 << 10) << int(rng.integers(0, 7)) for _ in range(20)]
+    descs, off = [], 0
+    for L in lens:
+        stride = (L + 255) // 256 * 256
+        descs.append([off, stride, L, 0])
+        off += 14 * stride
+    buf = torch.zeros(off, dtype=torch.uint8, device="cuda")
+    host = np.zeros(off, dtype=np.uint8)
+    for j, (o, st, L, _) in enumerate(descs):
+        for i in range(10):
+            host[o + i * st: o + i * st + L] = rng.integers(0, 256, L, dtype=np.uint8)
+    buf.copy_(torch.from_numpy(host))
+    B.encode_ragged(rs, buf, descs)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    for o, st, L, _ in descs:
+        data = np.stack([host[o + i * st: o + i * st + L] for i in range(10)])
+        ref = corc.encode_stripes(data[None].copy())[0]
+        for j in range(4):
+            assert np.array_equal(got[o + (10 + j) * st: o + (10 + j) * st + L], ref[j])
+    good = buf.clone()
+    full = (1 << 14) - 1
+    for d in descs:
+        e = rng.choice(14, int(rng.integers(0, 5)), replace=False)
+        d[3] = full & ~int(sum(1 << int(i) for i in e))
+        for i in e:
+            buf[d[0] + int(i) * d[1]: d[0] + int(i) * d[1] + d[2]] = 0x33
+    descs[0][3] = full & ~0b11111  # too few present: skipped + counted
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.reconstruct_ragged(rs, buf, descs, bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 1
+    for j, (o, st, L, m) in enumerate(descs):
+        if j == 0:
+            continue
+        assert torch.equal(buf[o: o + 14 * st], good[o: o + 14 * st]), j

@@ -182,6 +182,8 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
     for s, (o, st, L, _) in enumerate(descs):
         B.fill_splitmix(dev[o:o + K_DATA * L].view(1, 1, -1), K_DATA * L, rank_seed_base(rank) + s)
     data = int(sum(K_DATA * d[2] for d in descs))
+    # decode payload counts only stripes with an erasure (e = 0 is upstream's no-op)
+    dec_data = int(sum(K_DATA * d[2] for d in descs if d[3] != full))
     B.encode_ragged(rs, dev, descs)  # warm-up
     B.reconstruct_ragged(rs, dev, descs)
     torch.cuda.synchronize()
@@ -214,10 +216,11 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
         B.host_reconstruct_batch(rs, h, m)
     t_e2e = time.perf_counter() - t0
     return {"stripes": n_stripes, "shard_lens": "64 KiB..4 MiB log-uniform", "erasures": "0..4 uniform",
-            "payload_GiB": round(data / 2**30, 3),
-            "device_resident_data_GiB_s": round(2 * data / t_dev / 2**30, 2),
+            "payload_GiB": round((data + dec_data) / 2**30, 3),
+            "payload": "encode 10 L per stripe + decode 10 L per stripe with >= 1 erasure",
+            "device_resident_data_GiB_s": round((data + dec_data) / t_dev / 2**30, 2),
             "device_resident": "one ragged encode + one ragged reconstruct launch over all stripes",
-            "end_to_end_data_GiB_s": round(2 * data / t_e2e / 2**30, 2)}
+            "end_to_end_data_GiB_s": round((data + dec_data) / t_e2e / 2**30, 2)}
 
 
 def main():

@@ -290,3 +290,42 @@ def test_ragged_device_batch(gpu):
         if j == 0:
             continue
         assert torch.equal(buf[o: o + 14 * st], good[o: o + 14 * st]), j
+
+
+def test_concurrent_host_calls(gpu):
+    """Reentrancy (SURVEY §8b Threading): host-API calls from 8 threads at once,
+    mixed encode / reconstruct / batch reconstruct and different lengths."""
+    import threading
+    import helyim_amd as H
+    rs = H.ReedSolomon(10, 4)
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(1000 + t)
+            for it in range(6):
+                L = int(rng.integers(1, 200000))
+                data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(10)]
+                sh = data + [np.zeros(L, np.uint8) for _ in range(4)]
+                rs.encode(sh)
+                ref = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(4)]
+                corc.CReedSolomon(10, 4).encode(ref)
+                assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+                e = set(rng.choice(14, 4, replace=False).tolist())
+                got = [None if i in e else ref[i].copy() for i in range(14)]
+                if it % 2:
+                    rs.reconstruct(got)
+                else:
+                    st = [got]
+                    rs.reconstruct_batch(st)
+                    got = st[0]
+                assert all(np.array_equal(got[i], ref[i]) for i in range(14))
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append(repr(ex))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors

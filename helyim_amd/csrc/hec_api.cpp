@@ -224,6 +224,7 @@ int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
     int rc = gd->decode_dense.upload(hp, &lut, s);
     if (rc) return rc;
     gd->decode_dense.fast104 = is104;
+    gd->decode_dense.lut_bits = uint32_t(n);
     gd->decode_ready = true;
     return HEC_OK;
 }
@@ -248,6 +249,8 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
     a.lut = ps.lut;
     a.bad_count = bad;
     a.fast104 = ps.fast104 ? 1u : 0u;
+    a.mask_limit = ps.lut_bits ? ((1u << ps.lut_bits) - 1u) : 0u;
+    if (masks && !ps.lut) return fail(HEC_ERR_INVALID_ARGUMENT, "per-stripe masks need a decode LUT");
     const uint64_t align = uint64_t(reinterpret_cast<uintptr_t>(in_base)) | in_stripe | in_shard |
                            uint64_t(reinterpret_cast<uintptr_t>(out_base)) | out_stripe | out_shard;
     const bool aligned = (align % 16) == 0;
@@ -425,6 +428,11 @@ int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, in
 int hec_set_xcd_parts(int parts) {
     if (parts < 1 || parts > 1024) return fail(HEC_ERR_INVALID_ARGUMENT, "parts in 1..1024");
     launch_config().xcd_parts = parts;
+    return HEC_OK;
+}
+
+int hec_set_chunk_rotation(int on) {
+    launch_config().chunk_rot = on ? 1 : 0;
     return HEC_OK;
 }
 

@@ -52,6 +52,7 @@ struct DevicePlanSet {
     uint32_t* lut = nullptr;
     size_t cap_plans = 0, cap_tabs = 0, cap_idx = 0, cap_lut = 0;
     bool fast104 = false;  // RS(10,4) set with fixed 4-row tables (rs104_kernel eligible)
+    uint32_t lut_bits = 0; // total shards the LUT covers (2^lut_bits entries)
     int upload(const HostPlans& hp, const std::vector<uint32_t>* lut_host, hipStream_t s);
     void release();
 };

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
         const uint32_t chunk = uint32_t(item - uint64_t(stripe) * a.chunks_per_stripe);
         uint32_t pid = 0;
         if (a.masks) {
-            pid = as_const(a.lut)[as_const(a.masks)[stripe]];
+            pid = as_const(a.lut)[as_const(a.masks)[stripe] & a.mask_limit];
             if (pid == kNoPlan) {
                 if (chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
                 continue;
@@ -311,7 +311,11 @@ template <bool DEC, bool XORONLY>
 __global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
     const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
     const uint32_t stripe = item / a.chunks_per_stripe;
-    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
+    uint32_t chunk = item - stripe * a.chunks_per_stripe;
+    if (a.chunk_rot) {  // per-stripe hashed rotation of the chunk order (bijective per stripe)
+        chunk += (stripe * 0x9E3779B1u) >> 8;
+        chunk %= a.chunks_per_stripe;
+    }
     const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
     rs104_chunk<DEC, XORONLY>(a.in_base + uint64_t(stripe) * a.in_stripe, a.out_base + uint64_t(stripe) * a.out_stripe,
                               a.in_shard, a.out_shard, a.len, chunk, mask, as_const(a.tabs), as_const(a.lut),
@@ -352,6 +356,7 @@ static hipError_t launch_rs104(ApplyArgs a, const LaunchConfig& cfg, hipStream_t
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
+    a.chunk_rot = uint32_t(cfg.chunk_rot);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
     hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY>), dim3(uint32_t(a.n_items)), dim3(kThreads), lds, stream, a);
     return hipGetLastError();

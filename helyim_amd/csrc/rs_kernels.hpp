@@ -39,9 +39,11 @@ struct ApplyArgs {
     const uint32_t* idx;
     const uint32_t* masks;       // optional per-stripe present mask (bit i = shard i present)
     const uint32_t* lut;         // mask -> plan id (used when masks != nullptr)
+    uint32_t mask_limit;         // (1 << total shards) - 1: masks are clipped to the LUT
     uint32_t* bad_count;         // optional: stripes skipped for too few present shards
     uint32_t xcd_remap;          // 1: workgroups sharing an XCD take consecutive chunks
     uint32_t xcd_parts;          // with xcd_remap 1: regions per XCD worked on concurrently
+    uint32_t chunk_rot;          // 1: rotate each stripe's chunk order by a hash of the stripe id
     uint32_t fast104;            // 1: RS(10,4) plan set with 4-row tables; encode = plan 0 at
                                  //    offset 0, decode = tables at lut[mask] * 200 words
 };
@@ -80,6 +82,7 @@ struct LaunchConfig {
     int xcd_remap = 1;           // 0 none, 1 eighths, G>=2 runs of G chunks per XCD (speed only)
     int blocks_per_cu = 0;       // >0: cap resident workgroups per CU via dynamic LDS (0 = no cap)
     int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
+    int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees

@@ -234,6 +234,9 @@ int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, in
 /* With xcd_remap 1: the workgroups of one XCD work on `parts` regions of the
  * batch concurrently (1 = one contiguous eighth per XCD). Speed only. */
 int hec_set_xcd_parts(int parts);
+/* 1: each stripe walks its 4 KiB chunks starting at a hashed offset, so
+ * concurrently running stripes touch different column ranges. Speed only. */
+int hec_set_chunk_rotation(int on);
 /* Diagnostic: 0 = GF(2^8) coding (default); 1 = XOR-only bandwidth ceiling --
  * the RS(10,4) aligned kernel with its GF math replaced by plain XOR (same
  * loads, stores and addressing; WRONG parity by design), used only to measure

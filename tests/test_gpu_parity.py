@@ -329,3 +329,23 @@ def test_concurrent_host_calls(gpu):
     for th in ths:
         th.join()
     assert not errors, errors
+
+
+def test_masks_with_stray_high_bits(gpu):
+    """Present masks with bits above the shard count set are clipped, never
+    index past the decode LUT (generic geometry and RS(10,4) fast path)."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    for k, m in ((10, 4), (6, 3)):
+        rs = H.ReedSolomon(k, m)
+        n = k + m
+        S, L = 4, 4096
+        t = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device="cuda")
+        B.encode_batch(rs, t)
+        good = t.clone()
+        masks = torch.tensor([((1 << n) - 1) & ~1 | (0x7FFF0000)] * S, dtype=torch.int32, device="cuda")
+        t[:, 0] = 0
+        B.reconstruct_batch(rs, t, masks)
+        torch.cuda.synchronize()
+        assert torch.equal(t, good)

@@ -275,6 +275,22 @@ int Scratch::reserve(size_t bytes) {
     return HEC_OK;
 }
 
+int Scratch::reserve_host(size_t bytes) {
+    if (bytes <= hcap) return HEC_OK;
+    if (hbuf) HEC_HIP(hipHostFree(hbuf));
+    hbuf = nullptr;
+    hcap = 0;
+    size_t want = std::max(bytes, size_t(16) << 20);
+    HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&hbuf), want, hipHostMallocDefault));
+    hcap = want;
+    return HEC_OK;
+}
+
+uint64_t& host_staging_max() {
+    static uint64_t v = uint64_t(64) << 20;
+    return v;
+}
+
 int device_scratch(Scratch** out) {
     int dev;
     int rc = current_device(&dev);
@@ -313,16 +329,31 @@ static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* co
     std::lock_guard<std::mutex> lk(sc->mu);
     const uint64_t Lp = round_up(L, 256);
     if ((rc = sc->reserve(size_t(Lp) * rs->n))) return rc;
+    uint8_t* par = sc->dbuf + size_t(rs->k) * Lp;
+    auto dst_of = [&](int j) { return parity_out ? parity_out[j] : parity_vec->data() + size_t(j) * L; };
+    if (uint64_t(rs->k) * L <= host_staging_max()) {
+        // pinned staging: k shards packed -> one H2D, one D2H of the m parity rows
+        if ((rc = sc->reserve_host(size_t(Lp) * rs->n))) return rc;
+        parallel_for(size_t(rs->k), uint64_t(rs->k) * L,
+                     [&](size_t i) { std::memcpy(sc->hbuf + i * Lp, data[i], L); });
+        HEC_HIP(hipMemcpyAsync(sc->dbuf, sc->hbuf, size_t(rs->k) * Lp, hipMemcpyHostToDevice, sc->stream));
+        if ((rc = run_apply(gd->encode, uint32_t(rs->k), sc->dbuf, 0, Lp, par, 0, Lp, round_up(L, 16), 1,
+                            nullptr, nullptr, sc->stream)))
+            return rc;
+        uint8_t* hpar = sc->hbuf + size_t(rs->k) * Lp;
+        HEC_HIP(hipMemcpyAsync(hpar, par, size_t(rs->m - 1) * Lp + L, hipMemcpyDeviceToHost, sc->stream));
+        HEC_HIP(hipStreamSynchronize(sc->stream));
+        parallel_for(size_t(rs->m), uint64_t(rs->m) * L,
+                     [&](size_t j) { std::memcpy(dst_of(int(j)), hpar + j * Lp, L); });
+        return HEC_OK;
+    }
     for (int i = 0; i < rs->k; ++i)
         HEC_HIP(hipMemcpyAsync(sc->dbuf + i * Lp, data[i], L, hipMemcpyHostToDevice, sc->stream));
-    uint8_t* par = sc->dbuf + size_t(rs->k) * Lp;
     if ((rc = run_apply(gd->encode, uint32_t(rs->k), sc->dbuf, 0, Lp, par, 0, Lp, round_up(L, 16), 1,
                         nullptr, nullptr, sc->stream)))
         return rc;
-    for (int j = 0; j < rs->m; ++j) {
-        uint8_t* dst = parity_out ? parity_out[j] : parity_vec->data() + size_t(j) * L;
-        HEC_HIP(hipMemcpyAsync(dst, par + j * Lp, L, hipMemcpyDeviceToHost, sc->stream));
-    }
+    for (int j = 0; j < rs->m; ++j)
+        HEC_HIP(hipMemcpyAsync(dst_of(j), par + j * Lp, L, hipMemcpyDeviceToHost, sc->stream));
     HEC_HIP(hipStreamSynchronize(sc->stream));
     return HEC_OK;
 }
@@ -343,6 +374,9 @@ static int reconstruct_host(const hec_rs* rs, uint8_t* const* shards, const size
     }
     if (npresent == rs->n) return HEC_OK;
     if (npresent < rs->k) return HEC_ERR_TOO_FEW_SHARDS_PRESENT;
+    if (rs->k == 10 && rs->m == 4 && uint64_t(rs->k) * L <= host_staging_max())
+        // one-stripe degraded read: pinned compact staging + the dense-LUT kernel
+        return hec_rs_reconstruct_batch(rs, shards, lens, present, 1, data_only ? 1 : 0, nullptr);
     Mat coefs;
     std::vector<uint32_t> in_ids, out_ids;
     bool noop = false;
@@ -433,6 +467,11 @@ int hec_set_xcd_parts(int parts) {
 
 int hec_set_chunk_rotation(int on) {
     launch_config().chunk_rot = on ? 1 : 0;
+    return HEC_OK;
+}
+
+int hec_set_host_staging(uint64_t max_bytes) {
+    host_staging_max() = max_bytes;
     return HEC_OK;
 }
 

@@ -3,9 +3,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hec.h"
@@ -81,10 +83,34 @@ struct Scratch {
     hipStream_t stream = nullptr;
     uint8_t* dbuf = nullptr;
     size_t dcap = 0;
+    uint8_t* hbuf = nullptr;  // pinned staging for small calls (one H2D + one D2H)
+    size_t hcap = 0;
     DevicePlanSet adhoc;
     int reserve(size_t bytes);
+    int reserve_host(size_t bytes);
 };
 int device_scratch(Scratch** out);
+
+// Host calls whose k * shard_len input is at most this many bytes go through
+// pinned staging (one H2D, one D2H) instead of one pageable copy per shard.
+uint64_t& host_staging_max();
+
+// Run fn(i) for i in [0, n) on up to 16 threads (host memcpy of staging).
+template <typename F>
+void parallel_for(size_t n, uint64_t bytes, F fn) {
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = unsigned(std::min<uint64_t>(hw, std::max<uint64_t>(1, bytes >> 22)));  // >= 4 MiB/thread
+    if (nt <= 1 || n < 2) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = t; i < n; i += nt) fn(i);
+        });
+    for (auto& x : th) x.join();
+}
 
 // Run one plan set over a strided batch (plan 0 for every stripe unless masks).
 int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uint64_t in_stripe,

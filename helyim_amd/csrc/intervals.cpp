@@ -64,23 +64,6 @@ int ragged_scratch(RaggedScratch** out) {
     return HEC_OK;
 }
 
-// Run fn(i) for i in [0, n) on up to 16 threads (host memcpy of the packing).
-template <typename F>
-void parallel_for(size_t n, uint64_t bytes, F fn) {
-    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const unsigned nt = unsigned(std::min<uint64_t>(hw, std::max<uint64_t>(1, bytes >> 22)));  // >= 4 MiB/thread
-    if (nt <= 1 || n < 2) {
-        for (size_t i = 0; i < n; ++i) fn(i);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t)
-        th.emplace_back([&, t] {
-            for (size_t i = t; i < n; i += nt) fn(i);
-        });
-    for (auto& x : th) x.join();
-}
-
 }  // namespace
 }  // namespace hec
 

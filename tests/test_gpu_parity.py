@@ -85,6 +85,50 @@ def test_reconstruct_host_api_patterns(gpu):
         rs.reconstruct([None] * 5 + full[5:])
 
 
+@pytest.mark.parametrize("staging", ["off", "on", "edge"])
+@pytest.mark.parametrize("k,m", [(10, 4), (3, 2)])
+def test_host_calls_staged_and_direct(gpu, staging, k, m):
+    """hec_set_host_staging picks pinned staging (one H2D + one D2H) or one
+    pageable copy per shard; both give the oracle's bytes, including the
+    reconstruct_data contract."""
+    import helyim_amd as H
+    rng = np.random.default_rng(11 * k + m)
+    rs, ors = H.ReedSolomon(k, m), O.ReedSolomon(k, m)
+    try:
+        for L in (1, 17, 4096 + 3, 65536 + 7, (1 << 20) + 5):
+            lim = {"off": 0, "on": 1 << 40, "edge": k * L}[staging]
+            H.lib.hec_set_host_staging(lim)
+            data = [_rand(rng, L) for _ in range(k)]
+            sh = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+            ref = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+            rs.encode(sh)
+            ors.encode(ref)
+            for a, b in zip(sh, ref):
+                assert np.array_equal(a, b), (staging, L)
+            assert rs.verify(sh)
+            sh[k][L - 1] ^= 0x80
+            assert not rs.verify(sh)
+            for _ in range(3):
+                erased = set(rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False).tolist())
+                got = [None if i in erased else ref[i].copy() for i in range(k + m)]
+                rs.reconstruct(got)
+                for i in range(k + m):
+                    assert np.array_equal(got[i], ref[i]), (staging, L, sorted(erased), i)
+                got = [None if i in erased else ref[i].copy() for i in range(k + m)]
+                rs.reconstruct_data(got)
+                for i in range(k + m):
+                    if i in erased and i >= k:
+                        assert got[i] is None
+                    else:
+                        assert np.array_equal(got[i], ref[i])
+            with pytest.raises(H.TooFewShardsPresent):
+                rs.reconstruct([None] * (m + 1) + ref[m + 1:])
+            with pytest.raises(H.IncorrectShardSize):
+                rs.reconstruct([None, np.zeros(L + 1, np.uint8)] + ref[2:])
+    finally:
+        H.lib.hec_set_host_staging(64 << 20)
+
+
 def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):
     import torch
     import helyim_amd.batch as B

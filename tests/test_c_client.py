@@ -1,0 +1,47 @@
+"""The C ABI from a plain C process (no Python, no PyTorch in the client):
+tests/c/abi_client.c compiled with gcc against include/hec.h, linked to
+helyim_amd/libhec.so and the C oracle. This is the path a Rust `-sys` binding
+takes; the libhec in that process brings up the system HIP
+runtime itself."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _build(tmp_path):
+    lib = os.path.join(ROOT, "helyim_amd", "libhec.so")
+    orc = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+    if not (os.path.exists(lib) and os.path.exists(orc)):
+        pytest.fail("libhec.so / liboracle.so not built (run make)")
+    exe = str(tmp_path / "abi_client")
+    subprocess.run(["gcc", "-std=c99", "-O2", "-Wall", "-Werror", os.path.join(ROOT, "tests", "c", "abi_client.c"),
+                    "-I" + os.path.join(ROOT, "include"), "-L" + os.path.dirname(lib), "-lhec",
+                    "-L" + os.path.dirname(orc), "-loracle",
+                    "-Wl,-rpath," + os.path.dirname(lib) + ":" + os.path.dirname(orc), "-o", exe], check=True)
+    return exe
+
+
+def _gpu_present():
+    import torch
+    return torch.cuda.device_count() > 0  # counts without initialising HIP
+
+
+def test_c_client_without_device(tmp_path):
+    if _gpu_present():
+        pytest.skip("a GPU is present; the gpu-marked C client test covers this build")
+    exe = _build(tmp_path)
+    r = subprocess.run([exe, "nogpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_c_client_parity(gpu, tmp_path):
+    exe = _build(tmp_path)
+    env = dict(os.environ)
+    env.pop("HEC_LIB_PATH", None)
+    r = subprocess.run([exe, "gpu", str(tmp_path)], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "0 failed checks" in r.stdout

@@ -67,6 +67,13 @@ SIGNATURES = {
     "hec_find_data_filesize": (_I, [ctypes.c_char_p, ctypes.POINTER(_U64)]),
     "hec_write_data_file": (_I, [ctypes.c_char_p, ctypes.c_int64]),
     "hec_write_index_file_from_ec_index": (_I, [ctypes.c_char_p]),
+    "hec_locate_data": (_I, [_U64, _U64, _U64, _U64, _U64, _P, _S, ctypes.POINTER(_S)]),
+    "hec_interval_shard_id": (_U32, [_P]),
+    "hec_interval_offset": (_U64, [_P, _U64, _U64]),
+    "hec_find_needle_from_ecx": (_I, [ctypes.c_char_p, _U64, ctypes.POINTER(_U32), ctypes.POINTER(ctypes.c_int32)]),
+    "hec_read_ec_data": (_I, [ctypes.c_char_p, _U64, _U64, _P, _P, _S, _P]),
+    "hec_read_ec_needle": (_I, [ctypes.c_char_p, _U64, _P, _S, ctypes.POINTER(_S)]),
+    "hec_read_ec_needle_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64, _P, _S, ctypes.POINTER(_S)]),
     "hec_set_launch_config": (_I, [_I, ctypes.c_long, _I, _I]),
     "hec_set_kernel_mode": (_I, [_I]),
     "hec_set_host_staging": (_I, [ctypes.c_uint64]),

@@ -1,0 +1,332 @@
+// Needle reads from an EC volume: locate_data, the .ecx
+// needle lookup and the degraded read that rebuilds intervals of lost shards.
+//
+//   locate_data / Interval        <- helyim-ec/src/locate.rs:1-100
+//   find_needle_from_ecx          <- helyim-ec/src/volume/mod.rs:153-155, lib.rs:54-82
+//   locate_ec_shard_needle        <- helyim-ec/src/volume/mod.rs:136-151
+//   read_ec_shard_needle / _intervals / read_one_ec_shard_interval /
+//   recover_one_remote_ec_shard_interval
+//                                 <- helyim-store/src/erasure_coding/mod.rs:129-171,303-491
+//
+// The reference fetches other shards' intervals over gRPC; here the shards are
+// the local base.ecNN files (a lost shard is a missing file), which is the
+// same arithmetic with the network taken out. Every interval that needs
+// recovery in one call is rebuilt in one GPU batch (hec_rs_reconstruct_batch).
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hec_internal.hpp"
+
+namespace hec {
+namespace {
+
+constexpr uint64_t kDataShards = 10;  // DATA_SHARDS_COUNT
+constexpr int kTotalShards = 14;
+constexpr uint64_t kEntry = 16;  // NEEDLE_ENTRY_SIZE
+
+int io(const std::string& what) { return fail(HEC_ERR_IO, what + ": " + std::strerror(errno)); }
+
+uint64_t be64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+    return v;
+}
+uint32_t be32(const uint8_t* p) { return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3]; }
+
+std::string shard_name(const std::string& base, int id) {
+    char ext[8];
+    std::snprintf(ext, sizeof ext, ".ec%02d", id);
+    return base + ext;
+}
+
+// The base.ecNN files of one volume, opened once per call (missing = -1).
+struct Shards {
+    int fd[kTotalShards];
+    uint64_t size[kTotalShards];
+    Shards() {
+        for (int i = 0; i < kTotalShards; ++i) fd[i] = -1, size[i] = 0;
+    }
+    ~Shards() {
+        for (int f : fd)
+            if (f >= 0) ::close(f);
+    }
+    int open(const std::string& base) {
+        for (int i = 0; i < kTotalShards; ++i) {
+            const std::string name = shard_name(base, i);
+            fd[i] = ::open(name.c_str(), O_RDONLY);
+            if (fd[i] < 0) {
+                if (errno == ENOENT) continue;
+                return io("open " + name);
+            }
+            struct stat st;
+            if (::fstat(fd[i], &st) != 0) return io("stat " + name);
+            size[i] = uint64_t(st.st_size);
+        }
+        return HEC_OK;
+    }
+    // EcVolume::shards[0].ecd_filesize: the first loaded shard, ids ascending
+    int first() const {
+        for (int i = 0; i < kTotalShards; ++i)
+            if (fd[i] >= 0) return i;
+        return -1;
+    }
+};
+
+// pread until n bytes or EOF; returns bytes read or -1
+ssize_t pread_full(int fd, uint8_t* p, size_t n, uint64_t off) {
+    size_t got = 0;
+    while (got < n) {
+        ssize_t r = ::pread(fd, p + got, n - got, off_t(off + got));
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return -1;
+        }
+        if (r == 0) break;
+        got += size_t(r);
+    }
+    return ssize_t(got);
+}
+
+// locate_offset (locate.rs:74-94) + locate_offset_within_blocks (:96-100)
+void locate_offset(uint64_t large, uint64_t small, uint64_t data_size, uint64_t offset, uint64_t* block_index,
+                   bool* is_large, uint64_t* inner) {
+    const uint64_t large_row_size = large * kDataShards;
+    const uint64_t large_block_rows = data_size / (large * kDataShards);  // note: not locate_data's formula
+    if (offset < large_block_rows * large_row_size) {
+        *block_index = offset / large;
+        *inner = offset % large;
+        *is_large = true;
+        return;
+    }
+    offset -= large_block_rows * large_row_size;
+    *block_index = offset / small;
+    *inner = offset % small;
+    *is_large = false;
+}
+
+// locate_data (locate.rs:29-72)
+int locate(uint64_t large, uint64_t small, uint64_t data_size, uint64_t offset, uint64_t size,
+           std::vector<hec_interval>& out) {
+    if (large == 0 || small == 0) return fail(HEC_ERR_INVALID_ARGUMENT, "block sizes must be > 0");
+    uint64_t block_index, inner;
+    bool is_large;
+    locate_offset(large, small, data_size, offset, &block_index, &is_large, &inner);
+    const uint64_t large_block_rows = (data_size + small * kDataShards) / (large * kDataShards);
+    while (size > 0) {
+        hec_interval iv{block_index, inner, 0, large_block_rows, is_large ? 1u : 0u, 0u};
+        const uint64_t block_remaining = (is_large ? large : small) - inner;
+        if (size <= block_remaining) {
+            iv.size = size;
+            out.push_back(iv);
+            return HEC_OK;
+        }
+        iv.size = block_remaining;
+        out.push_back(iv);
+        size -= block_remaining;
+        block_index += 1;
+        if (is_large && block_index == large_block_rows * kDataShards) {
+            is_large = false;
+            block_index = 0;
+        }
+        inner = 0;
+    }
+    return HEC_OK;
+}
+
+uint64_t interval_offset(const hec_interval& iv, uint64_t large, uint64_t small) {
+    uint64_t off = iv.inner_block_offset;
+    const uint64_t row = iv.block_index / kDataShards;
+    if (iv.is_large_block)
+        off += row * large;
+    else
+        off += iv.large_block_rows * large + row * small;
+    return off;
+}
+
+const hec_rs* rs104() {
+    static hec_rs_t* rs = [] {
+        hec_rs_t* r = nullptr;
+        hec_rs_new(10, 4, &r);
+        return r;
+    }();
+    return rs;
+}
+
+// read_ec_shard_intervals over a list of (offset, size) ranges of the volume's
+// data: ranges are located, local intervals pread, lost ones rebuilt in one
+// batch. out receives the ranges' bytes back to back.
+int read_ranges(const std::string& base, uint64_t large, uint64_t small, const uint64_t* offsets,
+                const uint64_t* sizes, size_t n, uint8_t* out) {
+    Shards sh;
+    int rc = sh.open(base);
+    if (rc) return rc;
+    const int f = sh.first();
+    if (f < 0) return fail(HEC_ERR_SHARD_NOT_FOUND, "no .ecNN shard file for " + base);
+    const uint64_t data_size = sh.size[f] * kDataShards;  // volume/mod.rs:146
+    struct Lost {
+        int shard;
+        uint64_t off, size;
+        uint8_t* dst;
+    };
+    std::vector<Lost> lost;
+    std::vector<hec_interval> ivs;
+    uint8_t* dst = out;
+    for (size_t r = 0; r < n; ++r) {
+        ivs.clear();
+        if ((rc = locate(large, small, data_size, offsets[r], sizes[r], ivs))) return rc;
+        for (const hec_interval& iv : ivs) {
+            const int id = int(iv.block_index % kDataShards);
+            const uint64_t off = interval_offset(iv, large, small);
+            if (sh.fd[id] >= 0) {  // local shard: read_exact_at
+                const ssize_t got = pread_full(sh.fd[id], dst, iv.size, off);
+                if (got < 0) return io("read " + shard_name(base, id));
+                if (uint64_t(got) != iv.size)
+                    return fail(HEC_ERR_IO, "read " + shard_name(base, id) + ": failed to fill whole buffer");
+            } else {
+                lost.push_back({id, off, iv.size, dst});
+            }
+            dst += iv.size;
+        }
+    }
+    if (lost.empty()) return HEC_OK;
+    // recover_one_remote_ec_shard_interval: every other shard's read of the same
+    // range counts as present only at full length; reconstruct uses the first
+    // 10 present, so reading stops there (same bytes, fewer reads).
+    uint64_t arena_bytes = 0;
+    for (const Lost& l : lost) arena_bytes += uint64_t(kTotalShards) * l.size;
+    std::vector<uint8_t> arena(arena_bytes);
+    std::vector<uint8_t*> ptrs(lost.size() * kTotalShards);
+    std::vector<size_t> lens(lost.size() * kTotalShards);
+    std::vector<uint8_t> present(lost.size() * kTotalShards);
+    uint64_t at = 0;
+    for (size_t j = 0; j < lost.size(); ++j) {
+        const Lost& l = lost[j];
+        int np = 0;
+        for (int i = 0; i < kTotalShards; ++i) {
+            uint8_t* p = arena.data() + at + uint64_t(i) * l.size;
+            const size_t s = j * kTotalShards + i;
+            ptrs[s] = i == l.shard ? l.dst : p;
+            lens[s] = 0;
+            present[s] = 0;
+            if (i == l.shard || sh.fd[i] < 0 || np >= int(kDataShards)) continue;
+            const ssize_t got = pread_full(sh.fd[i], p, l.size, l.off);
+            if (got == ssize_t(l.size)) {
+                present[s] = 1;
+                lens[s] = l.size;
+                ++np;
+            }
+        }
+        at += uint64_t(kTotalShards) * l.size;
+    }
+    size_t bad = 0;
+    rc = hec_rs_reconstruct_batch(rs104(), ptrs.data(), lens.data(), present.data(), lost.size(), 1, &bad);
+    if (rc && bad < lost.size())
+        set_detail("recovering shard " + std::to_string(lost[bad].shard) + " interval at " +
+                   std::to_string(lost[bad].off) + ": " + hec_strerror(rc));
+    return rc;
+}
+
+}  // namespace
+}  // namespace hec
+
+using namespace hec;
+
+extern "C" {
+
+int hec_locate_data(uint64_t large_block_len, uint64_t small_block_len, uint64_t data_size, uint64_t offset,
+                    uint64_t size, hec_interval* out, size_t cap, size_t* n_out) {
+    if (!n_out || (cap && !out)) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    std::vector<hec_interval> ivs;
+    int rc = locate(large_block_len, small_block_len, data_size, offset, size, ivs);
+    if (rc) return rc;
+    *n_out = ivs.size();
+    if (ivs.size() > cap)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "need " + std::to_string(ivs.size()) + " intervals, cap " +
+                                                  std::to_string(cap));
+    std::copy(ivs.begin(), ivs.end(), out);
+    return HEC_OK;
+}
+
+uint32_t hec_interval_shard_id(const hec_interval* iv) { return iv ? uint32_t(iv->block_index % kDataShards) : 0; }
+
+uint64_t hec_interval_offset(const hec_interval* iv, uint64_t large_block_size, uint64_t small_block_size) {
+    return iv ? interval_offset(*iv, large_block_size, small_block_size) : 0;
+}
+
+int hec_find_needle_from_ecx(const char* base_filename, uint64_t needle_id, uint32_t* offset, int32_t* size) {
+    if (!base_filename || !offset || !size) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    const std::string name = std::string(base_filename) + ".ecx";
+    const int fd = ::open(name.c_str(), O_RDONLY);
+    if (fd < 0) return io("open " + name);
+    struct stat st;
+    if (::fstat(fd, &st) != 0) {
+        const int rc = io("stat " + name);
+        ::close(fd);
+        return rc;
+    }
+    uint64_t lo = 0, hi = uint64_t(st.st_size) / kEntry;
+    uint8_t e[kEntry];
+    int rc = -1;  // -1: not found
+    while (lo < hi && rc < 0) {
+        const uint64_t mid = (lo + hi) / 2;
+        const ssize_t got = pread_full(fd, e, kEntry, mid * kEntry);
+        if (got != ssize_t(kEntry)) {
+            rc = got < 0 ? io("read " + name) : fail(HEC_ERR_IO, "read " + name + ": failed to fill whole buffer");
+            break;
+        }
+        const uint64_t key = be64(e);
+        if (key == needle_id) {
+            *offset = be32(e + 8);
+            *size = int32_t(be32(e + 12));
+            rc = HEC_OK;
+        } else if (key < needle_id) {
+            lo = mid + 1;
+        } else {
+            hi = mid;
+        }
+    }
+    ::close(fd);
+    if (rc < 0) return fail(HEC_ERR_IO, "Needle " + std::to_string(needle_id) + " is not found");  // ErrorKind::NotFound
+    return rc;
+}
+
+int hec_read_ec_data(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                     const uint64_t* offsets, const uint64_t* sizes, size_t n_ranges, uint8_t* out) {
+    if (!base_filename || (n_ranges && (!offsets || !sizes || !out)))
+        return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    return read_ranges(base_filename, large_block_size, small_block_size, offsets, sizes, n_ranges, out);
+}
+
+int hec_read_ec_needle_ex(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                          uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out) {
+    if (!base_filename || !n_out) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    *n_out = 0;
+    uint32_t off;
+    int32_t sz;
+    int rc = hec_find_needle_from_ecx(base_filename, needle_id, &off, &sz);
+    if (rc) return rc;
+    if (sz < 0)  // Size::is_deleted
+        return fail(HEC_ERR_NEEDLE_NOT_FOUND, "Needle " + std::to_string(needle_id) + " not found");
+    const uint64_t actual_offset = uint64_t(uint32_t(off * 8u));  // Offset::actual_offset: u32 product
+    const uint32_t body = 16u + uint32_t(sz) + 4u;                  // Size::actual_size
+    const uint64_t actual_size = uint64_t(body + (8u - body % 8u));
+    *n_out = size_t(actual_size);
+    if (actual_size > cap)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "needle needs " + std::to_string(actual_size) + " bytes, cap " +
+                                                  std::to_string(cap));
+    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
+    return read_ranges(base_filename, large_block_size, small_block_size, &actual_offset, &actual_size, 1, out);
+}
+
+int hec_read_ec_needle(const char* base_filename, uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out) {
+    return hec_read_ec_needle_ex(base_filename, uint64_t(1) << 30, uint64_t(1) << 20, needle_id, out, cap, n_out);
+}
+
+}  // extern "C"

@@ -435,6 +435,8 @@ const char* hec_strerror(int status) {
         case HEC_ERR_UNDERFLOW: return "Only {0} shards found but {0} required";
         case HEC_ERR_UNEXPECTED_EC_SHARD_SIZE: return "ec shard size expected {0} but actually is {1}";
         case HEC_ERR_UNEXPECTED_BLOCK_SIZE: return "unexpected block size {0}, buffer size {1}";
+        case HEC_ERR_NEEDLE_NOT_FOUND: return "Needle not found in volume";
+        case HEC_ERR_SHARD_NOT_FOUND: return "Shard not found in volume";
         case HEC_ERR_HIP: return "HIP runtime error";
         case HEC_ERR_NO_DEVICE: return "no usable GPU device";
         case HEC_ERR_INVALID_ARGUMENT: return "invalid argument";

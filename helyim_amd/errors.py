@@ -6,6 +6,8 @@
   (/root/reference/helyim-ec/src/errors.rs:55-66), codes 32..35; an RS error
   raised from the file layer is wrapped as ``EcShardError.ErasureCoding``
   exactly like errors.rs:58-59 (``#[from] reed_solomon_erasure::Error``).
+* ``EcVolumeError`` subclasses mirror the needle-read variants of
+  helyim_ec::EcVolumeError (errors.rs:31-34), codes 48..49.
 * ``DeviceError`` covers this library's own HIP/device failures (64..).
 """
 from __future__ import annotations
@@ -44,6 +46,16 @@ class UnexpectedEcShardSize(EcShardError): code = 34
 class UnexpectedBlockSize(EcShardError): code = 35
 
 
+class EcVolumeError(Exception):
+    """helyim_ec::EcVolumeError (helyim-ec/src/errors.rs:15-35), the variants
+    the needle-read path returns."""
+    code = -1
+
+
+class NeedleNotFound(EcVolumeError): code = 48
+class ShardNotFound(EcVolumeError): code = 49
+
+
 class ErasureCoding(EcShardError):
     """EcShardError::ErasureCoding(reed_solomon_erasure::Error)"""
 
@@ -64,7 +76,8 @@ _RS = {c.code: c for c in (TooFewShards, TooManyShards, TooFewDataShards, TooMan
                            TooFewParityShards, TooManyParityShards, TooFewBufferShards,
                            TooManyBufferShards, IncorrectShardSize, TooFewShardsPresent,
                            EmptyShard, InvalidShardFlags, InvalidIndex)}
-_EC = {c.code: c for c in (Io, Underflow, UnexpectedEcShardSize, UnexpectedBlockSize)}
+_EC = {c.code: c for c in (Io, Underflow, UnexpectedEcShardSize, UnexpectedBlockSize, NeedleNotFound,
+                           ShardNotFound)}
 
 
 def _message(code: int) -> str:

@@ -56,6 +56,8 @@ enum hec_status {
     HEC_ERR_UNDERFLOW = 33,               /* EcShardError::Underflow */
     HEC_ERR_UNEXPECTED_EC_SHARD_SIZE = 34,/* EcShardError::UnexpectedEcShardSize */
     HEC_ERR_UNEXPECTED_BLOCK_SIZE = 35,   /* EcShardError::UnexpectedBlockSize */
+    HEC_ERR_NEEDLE_NOT_FOUND = 48,        /* EcVolumeError::NeedleNotFound */
+    HEC_ERR_SHARD_NOT_FOUND = 49,         /* EcVolumeError::ShardNotFound */
     HEC_ERR_HIP = 64,                     /* a HIP runtime call failed */
     HEC_ERR_NO_DEVICE = 65,               /* no usable GPU */
     HEC_ERR_INVALID_ARGUMENT = 66,        /* null pointer, bad stride, ... */
@@ -222,6 +224,53 @@ int hec_find_data_filesize(const char* base_filename, uint64_t* data_filesize);
 int hec_write_data_file(const char* base_filename, int64_t data_filesize);
 /* write_index_file_from_ec_index(base) (decoder.rs:22-44): .ecx + .ecj -> .idx. */
 int hec_write_index_file_from_ec_index(const char* base_filename);
+
+/* ---- needle reads from EC shards (locate + degraded read) ----------------- */
+/* Interval (helyim-ec/src/locate.rs:3-9). */
+typedef struct hec_interval {
+    uint64_t block_index;
+    uint64_t inner_block_offset;
+    uint64_t size;
+    uint64_t large_block_rows;
+    uint32_t is_large_block;
+    uint32_t reserved;
+} hec_interval;
+/* locate_data(large_block_len, small_block_len, data_size, offset, size)
+ * (locate.rs:29-72, with locate_offset :74-100 and its own large-row count).
+ * Writes up to cap intervals; *n_out = the number locate_data yields (an
+ * HEC_ERR_INVALID_ARGUMENT when it exceeds cap). */
+int hec_locate_data(uint64_t large_block_len, uint64_t small_block_len, uint64_t data_size, uint64_t offset,
+                    uint64_t size, hec_interval* out, size_t cap, size_t* n_out);
+/* Interval::shard_id (locate.rs:12-15) and Interval::offset (:17-27). */
+uint32_t hec_interval_shard_id(const hec_interval* interval);
+uint64_t hec_interval_offset(const hec_interval* interval, uint64_t large_block_size, uint64_t small_block_size);
+/* EcVolume::find_needle_from_ecx (volume/mod.rs:153-155 ->
+ * search_needle_from_sorted_index, lib.rs:54-82): binary search of base.ecx.
+ * *offset is the stored Offset (units of 8 bytes), *size the stored Size (< 0
+ * = deleted). Absent id -> HEC_ERR_IO ("Needle {id} is not found",
+ * io::ErrorKind::NotFound). */
+int hec_find_needle_from_ecx(const char* base_filename, uint64_t needle_id, uint32_t* offset, int32_t* size);
+/* read_ec_shard_intervals (erasure_coding/mod.rs:303-401) over n_ranges
+ * (offset, size) ranges of the volume's data, against the local shard files
+ * base.ec00..ec13 (data_size = first shard file's size x 10, volume/mod.rs:146).
+ * An interval on a present shard is read from it (short read -> HEC_ERR_IO);
+ * an interval on a missing shard is rebuilt from the other shards' same range
+ * (recover_one_remote_ec_shard_interval, :403-491: full-length reads count as
+ * present; fewer than 10 -> HEC_ERR_TOO_FEW_SHARDS_PRESENT). All rebuilt
+ * intervals of the call go to the GPU as one batch. out receives the ranges
+ * back to back (sum of sizes bytes). No shard file -> HEC_ERR_SHARD_NOT_FOUND. */
+int hec_read_ec_data(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                     const uint64_t* offsets, const uint64_t* sizes, size_t n_ranges, uint8_t* out);
+/* read_ec_shard_needle's data path (erasure_coding/mod.rs:129-171): look the
+ * needle up in base.ecx, HEC_ERR_NEEDLE_NOT_FOUND if deleted, then read its
+ * actual_size bytes at actual_offset (Offset * 8 as u32, Size::actual_size)
+ * through hec_read_ec_data with the 1 GiB / 1 MiB blocks. *n_out = the
+ * needle's byte count; cap smaller than that -> HEC_ERR_INVALID_ARGUMENT.
+ * Parsing the needle record is the caller's (Needle::read_bytes). */
+int hec_read_ec_needle(const char* base_filename, uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out);
+/* hec_read_ec_needle with explicit block sizes (tests exercise large rows). */
+int hec_read_ec_needle_ex(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                          uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out);
 
 /* ---- tuning / introspection ----------------------------------------------- */
 /* Kernel launch configuration (process-wide; speed only, results identical):

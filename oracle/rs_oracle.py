@@ -546,3 +546,132 @@ def write_index_file_from_ec_index(base: str) -> None:
             ids = open(base + ".ecj", "rb").read()
             for p in range(0, len(ids) - len(ids) % 8, 8):
                 out.write(ids[p:p + 8] + _struct.pack(">Ii", 0, -1))
+
+
+# --------------------------------------------------------------------------
+# Needle reads -- restated from the reference:
+#   locate_data / Interval      helyim-ec/src/locate.rs:1-100
+#   find_needle_from_ecx        helyim-ec/src/volume/mod.rs:153-155, lib.rs:54-82
+#   read path                   helyim-store/src/erasure_coding/mod.rs:129-171,303-491
+# Shards are the local base.ecNN files; a lost shard is a missing file.
+# --------------------------------------------------------------------------
+class NeedleNotFound(Exception):
+    pass
+
+
+class ShardNotFound(Exception):
+    pass
+
+
+def _locate_offset(large, small, data_size, offset):
+    """locate.rs:74-100 (large-row count = data_size // (large * 10))."""
+    large_row_size = large * DATA_SHARDS_COUNT
+    large_block_rows = data_size // (large * DATA_SHARDS_COUNT)
+    if offset < large_block_rows * large_row_size:
+        return offset // large, True, offset % large
+    offset -= large_block_rows * large_row_size
+    return offset // small, False, offset % small
+
+
+def locate_data(large, small, data_size, offset, size):
+    """locate.rs:29-72. Intervals as (block_index, inner_block_offset, size,
+    is_large_block, large_block_rows); note the large-row count here is
+    (data_size + small * 10) // (large * 10), unlike _locate_offset."""
+    block_index, is_large, inner = _locate_offset(large, small, data_size, offset)
+    large_block_rows = (data_size + small * DATA_SHARDS_COUNT) // (large * DATA_SHARDS_COUNT)
+    out = []
+    while size > 0:
+        remaining = (large if is_large else small) - inner
+        if size <= remaining:
+            out.append((block_index, inner, size, is_large, large_block_rows))
+            return out
+        out.append((block_index, inner, remaining, is_large, large_block_rows))
+        size -= remaining
+        block_index += 1
+        if is_large and block_index == large_block_rows * DATA_SHARDS_COUNT:
+            is_large, block_index = False, 0
+        inner = 0
+    return out
+
+
+def interval_shard_id(iv) -> int:
+    """Interval::shard_id (locate.rs:12-15)."""
+    return iv[0] % DATA_SHARDS_COUNT
+
+
+def interval_offset(iv, large, small) -> int:
+    """Interval::offset (locate.rs:17-27)."""
+    block_index, inner, _, is_large, large_block_rows = iv
+    row = block_index // DATA_SHARDS_COUNT
+    if is_large:
+        return inner + row * large
+    return inner + large_block_rows * large + row * small
+
+
+def find_needle_from_ecx(base: str, needle_id: int):
+    """search_needle_from_sorted_index (lib.rs:54-82): (offset, size) as stored."""
+    raw = open(base + ".ecx", "rb").read()
+    lo, hi = 0, len(raw) // 16
+    while lo < hi:
+        mid = (lo + hi) // 2
+        key, off, size = _struct.unpack(">QIi", raw[mid * 16:mid * 16 + 16])
+        if key == needle_id:
+            return off, size
+        if key < needle_id:
+            lo = mid + 1
+        else:
+            hi = mid
+    raise IoError("Needle %d is not found" % needle_id)
+
+
+def read_ec_data(base: str, ranges, large=ERASURE_CODING_LARGE_BLOCK_SIZE,
+                 small=ERASURE_CODING_SMALL_BLOCK_SIZE) -> bytes:
+    """read_ec_shard_intervals over (offset, size) ranges from the local shard
+    files: data_size = first shard file's size * 10 (volume/mod.rs:146); a
+    present shard is read exactly (read_exact_at, mod.rs:344); a missing one
+    is recovered from every other shard's full-length read of the same range
+    (mod.rs:403-491: read == buf_len) with upstream reconstruct."""
+    names = [base + to_ext(i) for i in range(TOTAL_SHARDS_COUNT)]
+    have = [os.path.exists(n) for n in names]
+    if not any(have):
+        raise ShardNotFound(base)
+    data_size = os.path.getsize(names[have.index(True)]) * DATA_SHARDS_COUNT
+    rs = ReedSolomon(DATA_SHARDS_COUNT, PARITY_SHARDS_COUNT)
+    out = bytearray()
+
+    def pread(i, off, n):
+        with open(names[i], "rb") as f:
+            f.seek(off)
+            return f.read(n)
+
+    for offset, size in ranges:
+        for iv in locate_data(large, small, data_size, offset, size):
+            sid, off, n = interval_shard_id(iv), interval_offset(iv, large, small), iv[2]
+            if have[sid]:
+                b = pread(sid, off, n)
+                if len(b) != n:
+                    raise IoError("UnexpectedEof")
+                out += b
+                continue
+            bufs = [None] * TOTAL_SHARDS_COUNT
+            for i in range(TOTAL_SHARDS_COUNT):
+                if i != sid and have[i]:
+                    b = pread(i, off, n)
+                    if len(b) == n:
+                        bufs[i] = np.frombuffer(b, np.uint8).copy()
+            rs.reconstruct(bufs)
+            out += bufs[sid].tobytes()
+    return bytes(out)
+
+
+def read_ec_needle(base: str, needle_id: int, large=ERASURE_CODING_LARGE_BLOCK_SIZE,
+                   small=ERASURE_CODING_SMALL_BLOCK_SIZE) -> bytes:
+    """read_ec_shard_needle's data path (mod.rs:129-171 via
+    locate_ec_shard_needle, volume/mod.rs:136-151)."""
+    off, size = find_needle_from_ecx(base, needle_id)
+    if size < 0:
+        raise NeedleNotFound(needle_id)
+    actual_offset = (off * 8) & 0xFFFFFFFF              # Offset::actual_offset, u32 product
+    body = 16 + (size & 0xFFFFFFFF) + 4                 # Size::actual_size
+    actual_size = (body + (8 - body % 8)) & 0xFFFFFFFF
+    return read_ec_data(base, [(actual_offset, actual_size)], large, small)

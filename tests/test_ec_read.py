@@ -1,0 +1,256 @@
+"""Needle reads from EC shards: locate_data, the .ecx
+lookup and the degraded read (helyim-ec/src/locate.rs,
+helyim-store/src/erasure_coding/mod.rs:129-491).
+
+The oracle's read path is pinned against the volume's own .dat bytes (a read
+of an intact or degraded volume must return the original data), and
+locate_data against intervals derived by hand from locate.rs. CPU tests cover
+everything that needs no reconstruction (libhec reads present shards without
+touching the GPU); gpu tests rebuild lost intervals and compare with the
+oracle."""
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle import rs_oracle as O
+
+LARGE, SMALL, BUF = 640, 32, 16
+
+
+def _volume(tmp_path, size, seed=3, name="v"):
+    base = str(tmp_path / name)
+    dat = O.splitmix64_bytes(seed, size).tobytes()
+    open(base + ".dat", "wb").write(dat)
+    assert corc.write_ec_files(base, BUF, LARGE, SMALL) == 0
+    return base, dat
+
+
+def _drop(base, ids):
+    import os
+    for i in ids:
+        os.remove(base + O.to_ext(i))
+
+
+def _ranges(rng, size, n, maxlen=3000):
+    out = []
+    for _ in range(n):
+        ln = int(rng.integers(1, maxlen))
+        off = int(rng.integers(0, max(size - ln, 1)))
+        out.append((off, min(ln, size - off)))
+    return out
+
+
+# ---- locate_data ------------------------------------------------------------
+
+# (large, small, data_size, offset, size) -> [(block_index, inner, size, is_large, large_block_rows)]
+LOCATE_KAT = [
+    # inside the large rows, across one block boundary
+    ((640, 32, 19520, 1000, 700), [(1, 360, 280, True, 3), (2, 0, 420, True, 3)]),
+    # large -> small transition (block_index wraps to 0 at large_block_rows * 10)
+    ((640, 32, 19520, 19100, 150), [(29, 540, 100, True, 3), (0, 0, 32, False, 3), (1, 0, 18, False, 3)]),
+    # the two large-row counts disagree (locate.rs:39-40 vs :84): 2 vs 3
+    ((640, 32, 18880, 12805, 10), [(0, 5, 10, False, 3)]),
+    ((640, 32, 19520, 77, 0), []),
+    # real geometry: 1 GiB / 1 MiB blocks, a 30 GB volume
+    ((1 << 30, 1 << 20, 30_000_000_000, 21_474_836_480 + 5, 2 << 20),
+     [(0, 5, (1 << 20) - 5, False, 2), (1, 0, 1 << 20, False, 2), (2, 0, 5, False, 2)]),
+]
+
+
+@pytest.mark.parametrize("args,want", LOCATE_KAT)
+def test_locate_data_known_answers(args, want):
+    import helyim_amd as H
+    assert O.locate_data(*args) == want
+    assert [iv.as_tuple() for iv in H.locate_data(*args)] == want
+
+
+def test_interval_offsets_known_answers():
+    import helyim_amd as H
+    ivs = H.locate_data(640, 32, 19520, 19100, 150)
+    assert [(iv.shard_id(), iv.offset(640, 32)) for iv in ivs] == [(9, 1820), (0, 1920), (1, 1920)]
+    (q,) = H.locate_data(640, 32, 18880, 12805, 10)
+    assert (q.shard_id(), q.offset(640, 32)) == (0, 1925)  # mirrors the reference (true place: 1285)
+
+
+def test_locate_data_random_vs_oracle():
+    import helyim_amd as H
+    rng = np.random.default_rng(9)
+    for _ in range(3000):
+        large, small = [(64, 8), (640, 32), (640, 64), (4096, 256), (1 << 30, 1 << 20)][int(rng.integers(0, 5))]
+        data_size = int(rng.integers(0, 60 * large))
+        offset = int(rng.integers(0, data_size + 1))
+        size = int(rng.integers(0, 40 * small + (2 * large if rng.random() < 0.3 else 0)))  # <= ~2k intervals
+        want = O.locate_data(large, small, data_size, offset, size)
+        got = H.locate_data(large, small, data_size, offset, size)
+        assert [iv.as_tuple() for iv in got] == want, (large, small, data_size, offset, size)
+        assert [iv.offset(large, small) for iv in got] == [O.interval_offset(w, large, small) for w in want]
+        assert [iv.shard_id() for iv in got] == [O.interval_shard_id(w) for w in want]
+
+
+# ---- .ecx lookup --------------------------------------------------------------
+
+def test_find_needle_from_ecx(tmp_path):
+    import helyim_amd as H
+    base = str(tmp_path / "v")
+    keys = sorted(set(np.random.default_rng(2).integers(1, 1 << 40, 300).tolist()))
+    raw = b"".join(struct.pack(">QIi", k, i + 1, (i * 37) % 5000 - (100 if i % 17 == 0 else 0))
+                   for i, k in enumerate(keys))
+    open(base + ".ecx", "wb").write(raw)
+    for i, k in enumerate(keys):
+        assert H.find_needle_from_ecx(base, k) == O.find_needle_from_ecx(base, k)
+    for k in (0, keys[0] - 1, keys[-1] + 1, keys[10] + 1):
+        if k in keys:
+            continue
+        with pytest.raises(H.Io, match="is not found"):
+            H.find_needle_from_ecx(base, k)
+        with pytest.raises(O.IoError):
+            O.find_needle_from_ecx(base, k)
+
+
+# ---- reads with every shard present (host only) ------------------------------
+
+@pytest.mark.parametrize("size", [19300, 6400 * 2 + 3, 1000, 32123])
+def test_oracle_read_matches_dat(tmp_path, size):
+    """Pins the oracle's read path: intact and degraded reads return the .dat."""
+    base, dat = _volume(tmp_path, size)
+    rng = np.random.default_rng(size)
+    ranges = _ranges(rng, size, 40)
+    want = b"".join(dat[o:o + n] for o, n in ranges)
+    assert O.read_ec_data(base, ranges, LARGE, SMALL) == want
+    _drop(base, [0, 3, 11, 13])
+    assert O.read_ec_data(base, ranges, LARGE, SMALL) == want
+
+
+@pytest.mark.parametrize("size", [19300, 32123])
+def test_read_present_shards_host_only(tmp_path, size):
+    import helyim_amd as H
+    base, dat = _volume(tmp_path, size)
+    _drop(base, [10, 11, 12, 13])  # parity lost: data reads need no reconstruction
+    rng = np.random.default_rng(size + 1)
+    ranges = _ranges(rng, size, 60)
+    assert H.read_ec_data(base, ranges, LARGE, SMALL) == b"".join(dat[o:o + n] for o, n in ranges)
+
+
+def test_read_quirk_volume_matches_oracle(tmp_path):
+    """locate.rs's two large-row counts disagree for this volume, so reads in
+    the small rows land past the shard ends; the product fails like the
+    oracle (read_exact_at -> UnexpectedEof) instead of returning bytes."""
+    import helyim_amd as H
+    base, dat = _volume(tmp_path, 6400 * 2 + 6000)
+    with pytest.raises(O.IoError):
+        O.read_ec_data(base, [(12800 + 5, 10)], LARGE, SMALL)
+    with pytest.raises(H.Io):
+        H.read_ec_data(base, [(12800 + 5, 10)], LARGE, SMALL)
+    assert H.read_ec_data(base, [(100, 1000)], LARGE, SMALL) == dat[100:1100]  # large rows are fine
+
+
+def test_read_errors_host_only(tmp_path):
+    import helyim_amd as H
+    with pytest.raises(H.ShardNotFound):
+        H.read_ec_data(str(tmp_path / "none"), [(0, 1)], LARGE, SMALL)
+    base, _ = _volume(tmp_path, 19300)
+    with open(base + O.to_ext(4), "r+b") as f:  # a present shard that is too short
+        f.truncate(100)
+    with pytest.raises(H.Io):
+        H.read_ec_data(base, [(4 * 640 + 200, 10)], LARGE, SMALL)
+
+
+def _needle_volume(tmp_path, n_needles=40, seed=4):
+    """A .dat with needles at 8-aligned offsets and its .idx -> .ecx."""
+    rng = np.random.default_rng(seed)
+    entries, pos = [], 8
+    for nid in range(1, n_needles + 1):
+        size = int(rng.integers(0, 900))
+        body = 16 + size + 4
+        actual = body + (8 - body % 8)
+        entries.append((nid * 7, pos // 8, size))
+        pos += actual
+    size = pos + 64
+    base, dat = _volume(tmp_path, size, seed=seed)
+    raw = b"".join(struct.pack(">QIi", k, o, s) for k, o, s in entries)
+    open(base + ".idx", "wb").write(raw)
+    O.write_sorted_file_from_index(base)
+    open(base + ".ecj", "wb").write(struct.pack(">Q", entries[5][0]))  # needle 6 deleted after EC
+    O.rebuild_ecx_file(base)
+    return base, dat, entries
+
+
+def _needle_bytes(dat, off, size):
+    body = 16 + size + 4
+    return dat[off * 8: off * 8 + body + (8 - body % 8)]
+
+
+def test_read_needles_host_only(tmp_path):
+    import helyim_amd as H
+    base, dat, entries = _needle_volume(tmp_path)
+    for i, (k, off, size) in enumerate(entries):
+        if i == 5:
+            with pytest.raises(H.NeedleNotFound):
+                H.read_ec_needle(base, k, LARGE, SMALL)
+            with pytest.raises(O.NeedleNotFound):
+                O.read_ec_needle(base, k, LARGE, SMALL)
+            continue
+        want = _needle_bytes(dat, off, size)
+        assert O.read_ec_needle(base, k, LARGE, SMALL) == want
+        assert H.read_ec_needle(base, k, LARGE, SMALL) == want
+    with pytest.raises(H.Io):
+        H.read_ec_needle(base, 123456789, LARGE, SMALL)
+
+
+# ---- degraded reads: lost data shards rebuilt on the GPU ---------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lost", [(0,), (2, 7), (0, 1, 2, 3), (9, 10, 12, 13), (4, 5, 6, 11)])
+def test_degraded_read_vs_oracle(gpu, tmp_path, lost):
+    import helyim_amd as H
+    size = 32123
+    base, dat = _volume(tmp_path, size)
+    _drop(base, lost)
+    rng = np.random.default_rng(sum(lost) + 1)
+    ranges = _ranges(rng, size, 300) + [(0, size), (size - 1, 1)]
+    want = b"".join(dat[o:o + n] for o, n in ranges)
+    got = H.read_ec_data(base, ranges, LARGE, SMALL)
+    assert got == want
+    assert O.read_ec_data(base, ranges[:40], LARGE, SMALL) == want[:sum(n for _, n in ranges[:40])]
+
+
+@pytest.mark.gpu
+def test_degraded_needle_reads(gpu, tmp_path):
+    import helyim_amd as H
+    base, dat, entries = _needle_volume(tmp_path, n_needles=120)
+    _drop(base, [1, 4, 8, 13])
+    for i, (k, off, size) in enumerate(entries):
+        if i == 5:
+            with pytest.raises(H.NeedleNotFound):
+                H.read_ec_needle(base, k, LARGE, SMALL)
+            continue
+        assert H.read_ec_needle(base, k, LARGE, SMALL) == _needle_bytes(dat, off, size), k
+
+
+@pytest.mark.gpu
+def test_degraded_read_default_geometry(gpu, tmp_path):
+    """1 GiB / 1 MiB blocks on a 3 MB volume (small rows only)."""
+    import helyim_amd as H
+    base = str(tmp_path / "v")
+    vol = O.synthetic_volume(3_000_000).tobytes()
+    open(base + ".dat", "wb").write(vol)
+    H.write_ec_files(base)
+    _drop(base, [0, 5, 9, 12])
+    rng = np.random.default_rng(8)
+    ranges = _ranges(rng, len(vol), 200, maxlen=300_000)
+    assert H.read_ec_data(base, ranges) == b"".join(vol[o:o + n] for o, n in ranges)
+
+
+@pytest.mark.gpu
+def test_degraded_read_too_many_lost(gpu, tmp_path):
+    import helyim_amd as H
+    base, dat = _volume(tmp_path, 19300)
+    _drop(base, [0, 1, 2, 3, 4])
+    assert H.read_ec_data(base, [(5 * 640 + 3, 600)], LARGE, SMALL) == dat[5 * 640 + 3:5 * 640 + 603]
+    with pytest.raises(H.ErasureCoding) as ei:
+        H.read_ec_data(base, [(100, 10)], LARGE, SMALL)
+    assert isinstance(ei.value.inner, H.TooFewShardsPresent)
+    with pytest.raises(O.RSError):
+        O.read_ec_data(base, [(100, 10)], LARGE, SMALL)

@@ -109,6 +109,44 @@ def cpu_baseline(seconds: float = 10.0) -> dict:
             "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
 
 
+def cpu_baseline_threads(seconds: float = 5.0, threads: int = 16) -> dict:
+    """the same C restatement, one thread per core over
+    independent stripes (ctypes drops the GIL inside the C calls). 16 threads
+    = the GPU box's CPU share per GPU."""
+    import threading
+    from oracle import corc
+    L = 1 << 20
+    rs = corc.CReedSolomon(K_DATA, M_PARITY)
+    simd = bool(corc.lib().orc_have_avx2())
+    counts = [0] * threads
+    stop = threading.Event()
+
+    def work(t):
+        rng = np.random.default_rng(100 + t)
+        d = corc.splitmix64_bytes(SEED_BASE + 1000 + t, K_DATA * L).reshape(K_DATA, L)
+        sh = [d[i].copy() for i in range(K_DATA)] + [np.zeros(L, np.uint8) for _ in range(M_PARITY)]
+        drop = sorted(rng.choice(N_TOTAL, 4, replace=False).tolist())
+        present = [i not in drop for i in range(N_TOTAL)]
+        while not stop.is_set():
+            rs.encode(sh, simd=simd)
+            rs.reconstruct(sh, present, simd=simd)
+            counts[t] += 1
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    time.sleep(seconds)
+    stop.set()
+    for x in th:
+        x.join()
+    el = time.perf_counter() - t0
+    n = sum(counts)
+    return {"value": round(n * 2 * K_DATA * L / 2**30 / el, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "sample": f"{n} stripe encode+decode passes over {threads} threads, one 1 MiB "
+                                      f"stripe per thread, {el:.1f} s"}
+
+
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -347,6 +385,7 @@ def main():
             out["mixed"] = mixed_section(rs, rank)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline_threads"] = cpu_baseline_threads(args.cpu_seconds / 2)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

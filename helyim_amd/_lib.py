@@ -74,6 +74,7 @@ SIGNATURES = {
     "hec_read_ec_data": (_I, [ctypes.c_char_p, _U64, _U64, _P, _P, _S, _P]),
     "hec_read_ec_needle": (_I, [ctypes.c_char_p, _U64, _P, _S, ctypes.POINTER(_S)]),
     "hec_read_ec_needle_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64, _P, _S, ctypes.POINTER(_S)]),
+    "hec_read_ec_needles": (_I, [ctypes.c_char_p, _U64, _U64, _P, _S, _P, _S, _P, _P]),
     "hec_set_launch_config": (_I, [_I, ctypes.c_long, _I, _I]),
     "hec_set_kernel_mode": (_I, [_I]),
     "hec_set_host_staging": (_I, [ctypes.c_uint64]),

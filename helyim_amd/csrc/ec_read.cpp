@@ -150,6 +150,54 @@ uint64_t interval_offset(const hec_interval& iv, uint64_t large, uint64_t small)
     return off;
 }
 
+// base.ecx opened for lookups: search_needle_from_sorted_index (lib.rs:54-82).
+struct Ecx {
+    int fd = -1;
+    uint64_t n = 0;
+    std::string name;
+    ~Ecx() {
+        if (fd >= 0) ::close(fd);
+    }
+    int open(const std::string& base) {
+        name = base + ".ecx";
+        fd = ::open(name.c_str(), O_RDONLY);
+        if (fd < 0) return io("open " + name);
+        struct stat st;
+        if (::fstat(fd, &st) != 0) return io("stat " + name);
+        n = uint64_t(st.st_size) / kEntry;
+        return HEC_OK;
+    }
+    // HEC_OK with the stored offset/size, -1 when absent, or an I/O status
+    int find(uint64_t id, uint32_t* offset, int32_t* size) const {
+        uint64_t lo = 0, hi = n;
+        uint8_t e[kEntry];
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            const ssize_t got = pread_full(fd, e, kEntry, mid * kEntry);
+            if (got != ssize_t(kEntry))
+                return got < 0 ? io("read " + name) : fail(HEC_ERR_IO, "read " + name + ": failed to fill whole buffer");
+            const uint64_t key = be64(e);
+            if (key == id) {
+                *offset = be32(e + 8);
+                *size = int32_t(be32(e + 12));
+                return HEC_OK;
+            }
+            if (key < id)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        return -1;
+    }
+};
+
+// Offset::actual_offset (u32 product) and Size::actual_size (needle.rs:49-74)
+uint64_t actual_offset(uint32_t off) { return uint64_t(uint32_t(off * 8u)); }
+uint64_t actual_size(int32_t sz) {
+    const uint32_t body = 16u + uint32_t(sz) + 4u;
+    return uint64_t(uint32_t(body + (8u - body % 8u)));
+}
+
 const hec_rs* rs104() {
     static hec_rs_t* rs = [] {
         hec_rs_t* r = nullptr;
@@ -262,37 +310,10 @@ uint64_t hec_interval_offset(const hec_interval* iv, uint64_t large_block_size, 
 
 int hec_find_needle_from_ecx(const char* base_filename, uint64_t needle_id, uint32_t* offset, int32_t* size) {
     if (!base_filename || !offset || !size) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    const std::string name = std::string(base_filename) + ".ecx";
-    const int fd = ::open(name.c_str(), O_RDONLY);
-    if (fd < 0) return io("open " + name);
-    struct stat st;
-    if (::fstat(fd, &st) != 0) {
-        const int rc = io("stat " + name);
-        ::close(fd);
-        return rc;
-    }
-    uint64_t lo = 0, hi = uint64_t(st.st_size) / kEntry;
-    uint8_t e[kEntry];
-    int rc = -1;  // -1: not found
-    while (lo < hi && rc < 0) {
-        const uint64_t mid = (lo + hi) / 2;
-        const ssize_t got = pread_full(fd, e, kEntry, mid * kEntry);
-        if (got != ssize_t(kEntry)) {
-            rc = got < 0 ? io("read " + name) : fail(HEC_ERR_IO, "read " + name + ": failed to fill whole buffer");
-            break;
-        }
-        const uint64_t key = be64(e);
-        if (key == needle_id) {
-            *offset = be32(e + 8);
-            *size = int32_t(be32(e + 12));
-            rc = HEC_OK;
-        } else if (key < needle_id) {
-            lo = mid + 1;
-        } else {
-            hi = mid;
-        }
-    }
-    ::close(fd);
+    Ecx ecx;
+    int rc = ecx.open(base_filename);
+    if (rc) return rc;
+    rc = ecx.find(needle_id, offset, size);
     if (rc < 0) return fail(HEC_ERR_IO, "Needle " + std::to_string(needle_id) + " is not found");  // ErrorKind::NotFound
     return rc;
 }
@@ -314,15 +335,52 @@ int hec_read_ec_needle_ex(const char* base_filename, uint64_t large_block_size, 
     if (rc) return rc;
     if (sz < 0)  // Size::is_deleted
         return fail(HEC_ERR_NEEDLE_NOT_FOUND, "Needle " + std::to_string(needle_id) + " not found");
-    const uint64_t actual_offset = uint64_t(uint32_t(off * 8u));  // Offset::actual_offset: u32 product
-    const uint32_t body = 16u + uint32_t(sz) + 4u;                  // Size::actual_size
-    const uint64_t actual_size = uint64_t(body + (8u - body % 8u));
-    *n_out = size_t(actual_size);
-    if (actual_size > cap)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "needle needs " + std::to_string(actual_size) + " bytes, cap " +
+    const uint64_t a_off = actual_offset(off), a_size = actual_size(sz);
+    *n_out = size_t(a_size);
+    if (a_size > cap)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "needle needs " + std::to_string(a_size) + " bytes, cap " +
                                                   std::to_string(cap));
     if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
-    return read_ranges(base_filename, large_block_size, small_block_size, &actual_offset, &actual_size, 1, out);
+    return read_ranges(base_filename, large_block_size, small_block_size, &a_off, &a_size, 1, out);
+}
+
+int hec_read_ec_needles(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                        const uint64_t* needle_ids, size_t n, uint8_t* out, size_t cap, uint64_t* out_offsets,
+                        int* statuses) {
+    if (!base_filename || !out_offsets || !statuses || (n && !needle_ids))
+        return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    Ecx ecx;
+    int rc = ecx.open(base_filename);
+    if (rc) return rc;
+    std::vector<uint64_t> offs, sizes;
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t off;
+        int32_t sz;
+        out_offsets[i] = total;
+        rc = ecx.find(needle_ids[i], &off, &sz);
+        if (rc > 0) return rc;  // I/O error on .ecx
+        if (rc < 0) {
+            statuses[i] = HEC_ERR_IO;  // not in .ecx (io::ErrorKind::NotFound)
+            continue;
+        }
+        if (sz < 0) {
+            statuses[i] = HEC_ERR_NEEDLE_NOT_FOUND;
+            continue;
+        }
+        statuses[i] = HEC_OK;
+        offs.push_back(actual_offset(off));
+        sizes.push_back(actual_size(sz));
+        total += sizes.back();
+    }
+    out_offsets[n] = total;
+    if (total > cap)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "needles need " + std::to_string(total) + " bytes, cap " +
+                                                  std::to_string(cap));
+    if (offs.empty()) return HEC_OK;
+    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
+    return read_ranges(base_filename, large_block_size, small_block_size, offs.data(), sizes.data(), offs.size(),
+                       out);
 }
 
 int hec_read_ec_needle(const char* base_filename, uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out) {

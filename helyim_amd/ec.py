@@ -162,3 +162,30 @@ def read_ec_needle(base_filename: str, needle_id: int, large_block_size: int = E
     check_ec(lib.hec_read_ec_needle_ex(name, large_block_size, small_block_size, needle_id, out, n.value,
                                        ctypes.byref(n)))
     return out.raw[:n.value]
+
+
+def read_ec_needles(base_filename: str, needle_ids, large_block_size: int = ERASURE_CODING_LARGE_BLOCK_SIZE,
+                    small_block_size: int = ERASURE_CODING_SMALL_BLOCK_SIZE):
+    """Many needle reads in one call (one GPU batch for every lost interval).
+    Returns one entry per id: the needle's bytes, or the exception the single
+    read would raise (``Io`` not in .ecx, ``NeedleNotFound`` deleted)."""
+    from .errors import _EC
+    ids = list(needle_ids)
+    n = len(ids)
+    c_ids = (ctypes.c_uint64 * max(n, 1))(*ids)
+    offs = (ctypes.c_uint64 * (n + 1))()
+    st = (ctypes.c_int * max(n, 1))()
+    name = base_filename.encode()
+    rc = lib.hec_read_ec_needles(name, large_block_size, small_block_size, c_ids, n, None, 0, offs, st)
+    if rc and not (n and offs[n] > 0):
+        check_ec(rc)
+    out = ctypes.create_string_buffer(max(offs[n], 1))
+    check_ec(lib.hec_read_ec_needles(name, large_block_size, small_block_size, c_ids, n, out, offs[n], offs, st))
+    raw = out.raw
+    res = []
+    for i in range(n):
+        if st[i]:
+            res.append(_EC[st[i]]("Needle %d: %s" % (ids[i], _lib.strerror(st[i]))))
+        else:
+            res.append(raw[offs[i]:offs[i + 1]])
+    return res

@@ -271,6 +271,17 @@ int hec_read_ec_needle(const char* base_filename, uint64_t needle_id, uint8_t* o
 /* hec_read_ec_needle with explicit block sizes (tests exercise large rows). */
 int hec_read_ec_needle_ex(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
                           uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out);
+/* Many needle reads of one volume in one call (a server's concurrent reads):
+ * every lost interval of every needle is rebuilt in one GPU batch.
+ * statuses[i] = HEC_OK, HEC_ERR_IO (id not in .ecx) or HEC_ERR_NEEDLE_NOT_FOUND
+ * (deleted); found needles' bytes go back to back into out, needle i at
+ * [out_offsets[i], out_offsets[i+1]) (empty when not found); out_offsets has
+ * n + 1 entries and is filled even when cap is too small (then
+ * HEC_ERR_INVALID_ARGUMENT). A shard read or reconstruct failure fails the
+ * whole call with that status. */
+int hec_read_ec_needles(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                        const uint64_t* needle_ids, size_t n, uint8_t* out, size_t cap, uint64_t* out_offsets,
+                        int* statuses);
 
 /* ---- tuning / introspection ----------------------------------------------- */
 /* Kernel launch configuration (process-wide; speed only, results identical):

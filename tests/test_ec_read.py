@@ -199,6 +199,21 @@ def test_read_needles_host_only(tmp_path):
         H.read_ec_needle(base, 123456789, LARGE, SMALL)
 
 
+def test_read_needles_batch_host_only(tmp_path):
+    import helyim_amd as H
+    base, dat, entries = _needle_volume(tmp_path)
+    ids = [k for k, _, _ in entries] + [999999, entries[3][0]]
+    got = H.read_ec_needles(base, ids, LARGE, SMALL)
+    for i, (k, off, size) in enumerate(entries):
+        if i == 5:
+            assert isinstance(got[i], H.NeedleNotFound)
+        else:
+            assert got[i] == _needle_bytes(dat, off, size)
+    assert isinstance(got[len(entries)], H.Io)
+    assert got[-1] == _needle_bytes(dat, entries[3][1], entries[3][2])
+    assert H.read_ec_needles(base, [], LARGE, SMALL) == []
+
+
 # ---- degraded reads: lost data shards rebuilt on the GPU ---------------------
 
 @pytest.mark.gpu
@@ -227,6 +242,19 @@ def test_degraded_needle_reads(gpu, tmp_path):
                 H.read_ec_needle(base, k, LARGE, SMALL)
             continue
         assert H.read_ec_needle(base, k, LARGE, SMALL) == _needle_bytes(dat, off, size), k
+
+
+@pytest.mark.gpu
+def test_degraded_needle_batch(gpu, tmp_path):
+    import helyim_amd as H
+    base, dat, entries = _needle_volume(tmp_path, n_needles=300, seed=6)
+    _drop(base, [0, 2, 3, 9])
+    got = H.read_ec_needles(base, [k for k, _, _ in entries], LARGE, SMALL)
+    for i, (k, off, size) in enumerate(entries):
+        if i == 5:
+            assert isinstance(got[i], H.NeedleNotFound)
+        else:
+            assert got[i] == _needle_bytes(dat, off, size), k
 
 
 @pytest.mark.gpu

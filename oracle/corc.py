@@ -51,6 +51,9 @@ def lib():
         L.orc_write_ec_files.restype = ctypes.c_int
         L.orc_rebuild_ec_files.argtypes = [ctypes.c_char_p, P, P, ctypes.c_int]
         L.orc_rebuild_ec_files.restype = ctypes.c_int
+        L.orc_read_ec_data.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, P, P, ctypes.c_size_t, P,
+                                       ctypes.c_int]
+        L.orc_read_ec_data.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -120,3 +123,17 @@ def rebuild_ec_files(base: str, simd: bool = True):
     rc = lib().orc_rebuild_ec_files(base.encode(), ctypes.cast(ids, ctypes.c_void_p),
                                     ctypes.cast(ctypes.pointer(n), ctypes.c_void_p), int(simd))
     return rc, [int(ids[i]) for i in range(n.value)]
+
+
+def read_ec_data(base: str, ranges, large: int = 1 << 30, small: int = 1 << 20, simd: bool = True):
+    """C restatement of the needle-interval read path (erasure_coding/mod.rs:303-491):
+    returns (rc, bytes); rc 0 ok, -1 io, -4 TooFewShardsPresent, -5 no shard."""
+    ranges = list(ranges)
+    n = len(ranges)
+    offs = np.array([r[0] for r in ranges] or [0], dtype=np.uint64)
+    sizes = np.array([r[1] for r in ranges] or [0], dtype=np.uint64)
+    total = int(sum(r[1] for r in ranges))
+    out = np.zeros(max(total, 1), dtype=np.uint8)
+    rc = lib().orc_read_ec_data(base.encode(), large, small, offs.ctypes.data, sizes.ctypes.data, n,
+                                out.ctypes.data, int(simd))
+    return rc, out[:total].tobytes()

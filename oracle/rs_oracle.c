@@ -383,3 +383,80 @@ int orc_rebuild_ec_files(const char* base, uint32_t* ids, size_t* n_ids, int sim
     orc_rs_free(rs);
     return rc;
 }
+
+/* orc_read_ec_data <- read_ec_shard_intervals / read_one_ec_shard_interval /
+ * recover_one_remote_ec_shard_interval (helyim-store/src/erasure_coding/
+ * mod.rs:303-491) with locate_data (helyim-ec/src/locate.rs:29-100), against
+ * the local base.ecNN files, one interval at a time like helyim: a present
+ * shard is read exactly; a missing one reads the same range from every other
+ * shard (full-length reads count as present) and runs upstream reconstruct.
+ * data_size = first shard file's size * 10 (volume/mod.rs:146).
+ * Returns 0, -1 io / short read, -4 TooFewShardsPresent, -5 no shard file. */
+int orc_read_ec_data(const char* base, uint64_t large, uint64_t small, const uint64_t* offsets,
+                     const uint64_t* sizes, size_t n, uint8_t* out, int simd) {
+    char name[4096];
+    int fd[14];
+    uint64_t data_size = 0;
+    int first = -1;
+    for (int i = 0; i < 14; i++) {
+        snprintf(name, sizeof name, "%s.ec%02d", base, i);
+        fd[i] = open(name, O_RDONLY);
+        if (fd[i] >= 0 && first < 0) {
+            struct stat st;
+            fstat(fd[i], &st);
+            data_size = (uint64_t)st.st_size * 10;
+            first = i;
+        }
+    }
+    if (first < 0) return -5;
+    void* rs = orc_rs_new(10, 4);
+    int rc = 0;
+    for (size_t r = 0; r < n && rc == 0; r++) {
+        /* locate_offset: its own large-row count (locate.rs:84) */
+        uint64_t off = offsets[r], size = sizes[r];
+        const uint64_t lrows_off = data_size / (large * 10);
+        uint64_t block, inner;
+        int is_large;
+        if (off < lrows_off * large * 10) {
+            block = off / large; inner = off % large; is_large = 1;
+        } else {
+            off -= lrows_off * large * 10;
+            block = off / small; inner = off % small; is_large = 0;
+        }
+        const uint64_t lrows = (data_size + small * 10) / (large * 10); /* locate.rs:39-40 */
+        while (size > 0 && rc == 0) {
+            const uint64_t remaining = (is_large ? large : small) - inner;
+            const uint64_t take = size <= remaining ? size : remaining;
+            const int sid = (int)(block % 10);
+            const uint64_t row = block / 10;
+            const uint64_t at = is_large ? inner + row * large : inner + lrows * large + row * small;
+            if (fd[sid] >= 0) {
+                size_t got = 0;
+                if (read_full(fd[sid], out, take, (off_t)at, &got) || got != take) rc = -1;
+            } else {
+                uint8_t* bufs[14];
+                uint8_t pres[14];
+                for (int i = 0; i < 14; i++) {
+                    bufs[i] = (uint8_t*)calloc(1, take);
+                    pres[i] = 0;
+                    if (i == sid || fd[i] < 0) continue;
+                    size_t got = 0;
+                    if (read_full(fd[i], bufs[i], take, (off_t)at, &got) == 0 && got == take) pres[i] = 1;
+                }
+                if (orc_reconstruct(rs, bufs, pres, take, 0, simd)) rc = -4;
+                else memcpy(out, bufs[sid], take);
+                for (int i = 0; i < 14; i++) free(bufs[i]);
+            }
+            out += take;
+            size -= take;
+            if (size == 0) break;
+            block += 1;
+            if (is_large && block == lrows * 10) { is_large = 0; block = 0; }
+            inner = 0;
+        }
+    }
+    for (int i = 0; i < 14; i++)
+        if (fd[i] >= 0) close(fd[i]);
+    orc_rs_free(rs);
+    return rc;
+}

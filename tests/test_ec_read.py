@@ -119,8 +119,10 @@ def test_oracle_read_matches_dat(tmp_path, size):
     ranges = _ranges(rng, size, 40)
     want = b"".join(dat[o:o + n] for o, n in ranges)
     assert O.read_ec_data(base, ranges, LARGE, SMALL) == want
+    assert corc.read_ec_data(base, ranges, LARGE, SMALL) == (0, want)
     _drop(base, [0, 3, 11, 13])
     assert O.read_ec_data(base, ranges, LARGE, SMALL) == want
+    assert corc.read_ec_data(base, ranges, LARGE, SMALL) == (0, want)
 
 
 @pytest.mark.parametrize("size", [19300, 32123])

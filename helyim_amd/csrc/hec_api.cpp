@@ -472,6 +472,13 @@ int hec_set_chunk_rotation(int on) {
     return HEC_OK;
 }
 
+int hec_set_workgroup_size(int threads) {
+    if (threads != 256 && threads != 512 && threads != 1024)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "workgroup size must be 256, 512 or 1024");
+    launch_config().wg_threads = threads;
+    return HEC_OK;
+}
+
 int hec_set_host_staging(uint64_t max_bytes) {
     host_staging_max() = max_bytes;
     return HEC_OK;

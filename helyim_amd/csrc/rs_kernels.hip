@@ -242,7 +242,7 @@ __device__ __forceinline__ uint32_t remap_block(uint32_t b, uint32_t nb, uint32_
 // One 4 KiB chunk of one RS(10,4) stripe. Encode (DEC=false): inputs 0..9 at
 // in_b, outputs 0..3 at out_b. Decode (DEC=true): in place at in_b == out_b,
 // shard ids from the present mask, tables at lut[mask] * 200 words.
-template <bool DEC, bool XORONLY, bool COMPACT = false>
+template <bool DEC, bool XORONLY, bool COMPACT = false, int TB = kThreads>
 __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
                                             uint64_t out_shard, uint64_t len, uint32_t chunk, uint32_t mask_in,
                                             cu32p tab, cu32p lut, uint32_t* bad_count) {
@@ -277,7 +277,7 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
 #pragma unroll
         for (int r = 0; r < R; ++r) out_id[r] = r;
     }
-    const uint64_t o = uint64_t(chunk) * (kThreads * kVecBytes) + threadIdx.x * kVecBytes;
+    const uint64_t o = uint64_t(chunk) * (TB * kVecBytes) + threadIdx.x * kVecBytes;
     if (o >= len) return;
     const uint64_t avail = len - o;
     u32x4 acc[R];
@@ -307,8 +307,8 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
     }
 }
 
-template <bool DEC, bool XORONLY>
-__global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
+template <bool DEC, bool XORONLY, int TB>
+__global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
     const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
     const uint32_t stripe = item / a.chunks_per_stripe;
     uint32_t chunk = item - stripe * a.chunks_per_stripe;
@@ -317,7 +317,8 @@ __global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
         chunk %= a.chunks_per_stripe;
     }
     const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
-    rs104_chunk<DEC, XORONLY>(a.in_base + uint64_t(stripe) * a.in_stripe, a.out_base + uint64_t(stripe) * a.out_stripe,
+    rs104_chunk<DEC, XORONLY, false, TB>(a.in_base + uint64_t(stripe) * a.in_stripe,
+                                         a.out_base + uint64_t(stripe) * a.out_stripe,
                               a.in_shard, a.out_shard, a.len, chunk, mask, as_const(a.tabs), as_const(a.lut),
                               a.bad_count);
 }
@@ -348,9 +349,9 @@ hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t str
     return hipGetLastError();
 }
 
-template <bool DEC, bool XORONLY>
-static hipError_t launch_rs104(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(kThreads) * kVecBytes;
+template <bool DEC, bool XORONLY, int TB>
+static hipError_t launch_rs104_tb(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
+    const uint64_t chunk = uint64_t(TB) * kVecBytes;
     a.chunks_per_stripe = uint32_t((a.len + chunk - 1) / chunk);
     a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
     if (a.n_items == 0) return hipSuccess;
@@ -358,8 +359,19 @@ static hipError_t launch_rs104(ApplyArgs a, const LaunchConfig& cfg, hipStream_t
     a.xcd_parts = uint32_t(cfg.xcd_parts);
     a.chunk_rot = uint32_t(cfg.chunk_rot);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY>), dim3(uint32_t(a.n_items)), dim3(kThreads), lds, stream, a);
+    hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY, TB>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
     return hipGetLastError();
+}
+
+// Workgroup size (speed only): 256 threads = one 4 KiB chunk per workgroup
+// (default); 512 / 1024 give each workgroup 8 / 16 KiB contiguous per shard.
+template <bool DEC, bool XORONLY>
+static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
+    switch (cfg.wg_threads) {
+        case 512: return launch_rs104_tb<DEC, XORONLY, 512>(a, cfg, stream);
+        case 1024: return launch_rs104_tb<DEC, XORONLY, 1024>(a, cfg, stream);
+        default: return launch_rs104_tb<DEC, XORONLY, kThreads>(a, cfg, stream);
+    }
 }
 
 template <int K, int U, bool ALIGNED, bool XORONLY = false>

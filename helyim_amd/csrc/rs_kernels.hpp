@@ -83,6 +83,7 @@ struct LaunchConfig {
     int blocks_per_cu = 0;       // >0: cap resident workgroups per CU via dynamic LDS (0 = no cap)
     int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
     int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
+    int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees

@@ -302,6 +302,9 @@ int hec_set_chunk_rotation(int on);
  * loads, stores and addressing; WRONG parity by design), used only to measure
  * the achievable HBM rate of this access pattern. Returns HEC_OK. */
 int hec_set_kernel_mode(int mode);
+/* Workgroup size of the RS(10,4) kernel: 256 (default; one 4 KiB chunk per
+ * workgroup), 512 or 1024 (8 / 16 KiB per shard per workgroup). Speed only. */
+int hec_set_workgroup_size(int threads);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables

@@ -160,12 +160,13 @@ def test_batch_encode_vs_oracle(gpu, L):
     assert np.array_equal(host[:, 10:], ref)
 
 
-@pytest.mark.parametrize("vec,max_blocks,remap,bpc", [
-    (1, 0, 0, 0), (1, 0, 1, 0), (1, 0, 16, 0), (1, 0, 256, 3), (1, 97, 1, 0),
-    (2, 0, 1, 0), (2, 97, 0, 0), (4, 0, 64, 0), (4, 97, 1, 2)])
-def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc):
+@pytest.mark.parametrize("vec,max_blocks,remap,bpc,wg", [
+    (1, 0, 0, 0, 256), (1, 0, 1, 0, 256), (1, 0, 16, 0, 256), (1, 0, 256, 3, 256), (1, 97, 1, 0, 256),
+    (2, 0, 1, 0, 256), (2, 97, 0, 0, 256), (4, 0, 64, 0, 256), (4, 97, 1, 2, 256),
+    (1, 0, 1, 0, 512), (1, 0, 0, 0, 1024), (1, 0, 1, 2, 1024)])
+def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc, wg):
     """Every launch configuration (fast and generic kernels, XCD remaps,
-    occupancy caps) produces identical encode and decode bytes."""
+    occupancy caps, workgroup sizes) produces identical encode and decode bytes."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -181,6 +182,7 @@ def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc):
                       for _ in range(S)], dtype=np.int32)
     try:
         B.set_launch_config(vec, max_blocks, remap, bpc)
+        assert H.lib.hec_set_workgroup_size(wg) == 0
         B.encode_batch(rs, t)
         torch.cuda.synchronize()
         assert torch.equal(t, ref)
@@ -195,6 +197,7 @@ def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc):
         assert torch.equal(t, ref)
     finally:
         B.set_launch_config()
+        H.lib.hec_set_workgroup_size(256)
 
 
 def test_batch_encode_separate_and_unaligned(gpu):

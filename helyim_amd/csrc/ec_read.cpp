@@ -244,41 +244,34 @@ int read_ranges(const std::string& base, uint64_t large, uint64_t small, const u
         }
     }
     if (lost.empty()) return HEC_OK;
-    // recover_one_remote_ec_shard_interval: every other shard's read of the same
-    // range counts as present only at full length; reconstruct uses the first
-    // 10 present, so reading stops there (same bytes, fewer reads).
-    uint64_t arena_bytes = 0;
-    for (const Lost& l : lost) arena_bytes += uint64_t(kTotalShards) * l.size;
-    std::vector<uint8_t> arena(arena_bytes);
-    std::vector<uint8_t*> ptrs(lost.size() * kTotalShards);
-    std::vector<size_t> lens(lost.size() * kTotalShards);
-    std::vector<uint8_t> present(lost.size() * kTotalShards);
-    uint64_t at = 0;
+    // recover_one_remote_ec_shard_interval: another shard counts as present when
+    // its read of the same range returns the full length, i.e. its file reaches
+    // off + size. The decode reads the first 10 of them, pread straight into
+    // pinned staging; the rebuilt interval is copied to its place in out.
+    std::vector<CompactJob> jobs(lost.size());
     for (size_t j = 0; j < lost.size(); ++j) {
         const Lost& l = lost[j];
-        int np = 0;
-        for (int i = 0; i < kTotalShards; ++i) {
-            uint8_t* p = arena.data() + at + uint64_t(i) * l.size;
-            const size_t s = j * kTotalShards + i;
-            ptrs[s] = i == l.shard ? l.dst : p;
-            lens[s] = 0;
-            present[s] = 0;
-            if (i == l.shard || sh.fd[i] < 0 || np >= int(kDataShards)) continue;
-            const ssize_t got = pread_full(sh.fd[i], p, l.size, l.off);
-            if (got == ssize_t(l.size)) {
-                present[s] = 1;
-                lens[s] = l.size;
-                ++np;
-            }
-        }
-        at += uint64_t(kTotalShards) * l.size;
+        uint32_t mask = 0;
+        for (int i = 0; i < kTotalShards; ++i)
+            if (i != l.shard && sh.fd[i] >= 0 && sh.size[i] >= l.off + l.size) mask |= 1u << i;
+        if (__builtin_popcount(mask) < int(kDataShards))
+            return fail(HEC_ERR_TOO_FEW_SHARDS_PRESENT, "recovering shard " + std::to_string(l.shard) +
+                                                            " interval at " + std::to_string(l.off) + ": " +
+                                                            std::to_string(__builtin_popcount(mask)) +
+                                                            " shards present");
+        jobs[j] = CompactJob{l.size, mask};
     }
-    size_t bad = 0;
-    rc = hec_rs_reconstruct_batch(rs104(), ptrs.data(), lens.data(), present.data(), lost.size(), 1, &bad);
-    if (rc && bad < lost.size())
-        set_detail("recovering shard " + std::to_string(lost[bad].shard) + " interval at " +
-                   std::to_string(lost[bad].off) + ": " + hec_strerror(rc));
-    return rc;
+    return compact_reconstruct_104(
+        rs104(), jobs,
+        [&](size_t j, int, int shard, uint8_t* dst) {
+            const ssize_t got = pread_full(sh.fd[shard], dst, lost[j].size, lost[j].off);
+            if (got == ssize_t(lost[j].size)) return int(HEC_OK);
+            return got < 0 ? io("read " + shard_name(base, shard))
+                           : fail(HEC_ERR_IO, "read " + shard_name(base, shard) + ": shard shrank during the read");
+        },
+        [&](size_t j, int shard, const uint8_t* src) {
+            if (shard == lost[j].shard) std::memcpy(lost[j].dst, src, lost[j].size);
+        });
 }
 
 }  // namespace

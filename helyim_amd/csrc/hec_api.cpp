@@ -287,7 +287,7 @@ int Scratch::reserve_host(size_t bytes) {
 }
 
 uint64_t& host_staging_max() {
-    static uint64_t v = uint64_t(64) << 20;
+    static uint64_t v = uint64_t(4) << 20;  // measured crossover
     return v;
 }
 

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -94,6 +95,21 @@ int device_scratch(Scratch** out);
 // Host calls whose k * shard_len input is at most this many bytes go through
 // pinned staging (one H2D, one D2H) instead of one pageable copy per shard.
 uint64_t& host_staging_max();
+
+// Batched RS(10,4) reconstruct of independent stripes through pinned compact
+// staging and one rs104_ragged_kernel launch (intervals.cpp). Job j has shard
+// length len and present mask; the decode reads its first 10 present shards,
+// which fill(j, slot, shard, dst) writes (len bytes) straight into staging
+// (non-zero return = that status aborts the call); take(j, shard, src) then
+// receives every erased shard. fill / take run on up to 16 threads.
+struct CompactJob {
+    uint64_t len;
+    uint32_t mask;
+};
+using CompactFill = std::function<int(size_t job, int slot, int shard, uint8_t* dst)>;
+using CompactTake = std::function<void(size_t job, int shard, const uint8_t* src)>;
+int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& jobs, const CompactFill& fill,
+                            const CompactTake& take);
 
 // Run fn(i) for i in [0, n) on up to 16 threads (host memcpy of staging).
 template <typename F>

@@ -5,6 +5,7 @@
 // GPU once, decoded by rs104_ragged_kernel (one workgroup per 4 KiB chunk of
 // each stripe, per-stripe length and erasure pattern), and copied back once.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -65,6 +66,88 @@ int ragged_scratch(RaggedScratch** out) {
 }
 
 }  // namespace
+
+int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& jobs, const CompactFill& fill,
+                            const CompactTake& take) {
+    const int k = rs->k, n = rs->n;
+    struct Lay {
+        uint64_t Lp, off, out_off;
+    };
+    std::vector<Lay> lay(jobs.size());
+    uint64_t total = 0;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        if (__builtin_popcount(jobs[j].mask) < k || jobs[j].len == 0 || jobs[j].len > 0xFFFFFFFFull)
+            return fail(HEC_ERR_INVALID_ARGUMENT, "compact job without k survivors");
+        lay[j].Lp = (jobs[j].len + 15) / 16 * 16;
+        lay[j].off = total;
+        total += (uint64_t(k) * lay[j].Lp + 255) / 256 * 256;  // compact inputs: the first k present shards
+    }
+    if (jobs.empty()) return HEC_OK;
+    const uint64_t in_total = total;
+    for (size_t j = 0; j < jobs.size(); ++j) {  // compact outputs: the erased shards, ascending
+        lay[j].out_off = total;
+        total += (uint64_t(n - __builtin_popcount(jobs[j].mask)) * lay[j].Lp + 255) / 256 * 256;
+    }
+    GeomDevice* gd;
+    int rc = geom_device(rs, &gd);
+    if (rc) return rc;
+    RaggedScratch* sc;
+    if ((rc = ragged_scratch(&sc))) return rc;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    std::vector<RaggedItem> items(jobs.size());
+    std::vector<uint32_t> block_item;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        const uint32_t chunks = uint32_t((jobs[j].len + 4095) / 4096);
+        items[j] = RaggedItem{lay[j].off, lay[j].Lp, uint32_t(jobs[j].len), jobs[j].mask,
+                              uint32_t(block_item.size()), 0, lay[j].out_off};
+        block_item.insert(block_item.end(), chunks, uint32_t(j));
+    }
+    const size_t items_bytes = items.size() * sizeof(RaggedItem);
+    const size_t meta = (items_bytes + 255) / 256 * 256 + block_item.size() * 4;
+    if ((rc = sc->reserve(total, meta))) return rc;
+    if ((rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
+    // survivors the decode reads (the first k present shards) -> slots 0..k-1
+    std::atomic<int> first_err{HEC_OK};
+    parallel_for(jobs.size(), in_total, [&](size_t j) {
+        int used = 0;
+        for (int i = 0; i < n && used < k; ++i)
+            if ((jobs[j].mask >> i) & 1) {
+                const int r = fill(j, used, i, sc->host + lay[j].off + used * lay[j].Lp);
+                if (r) {
+                    int expect = HEC_OK;
+                    first_err.compare_exchange_strong(expect, r);
+                    return;
+                }
+                ++used;
+            }
+    });
+    if (first_err.load()) return first_err.load();
+    std::memcpy(sc->hmeta, items.data(), items_bytes);
+    const size_t map_off = (items_bytes + 255) / 256 * 256;
+    std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
+    HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, sc->stream));
+    HEC_HIP(hipMemcpyAsync(sc->dev, sc->host, in_total, hipMemcpyHostToDevice, sc->stream));
+    RaggedArgs ra{};
+    ra.base = sc->dev;
+    ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
+    ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
+    ra.n_blocks = uint32_t(block_item.size());
+    ra.tabs = gd->decode_dense.tabs;
+    ra.lut = gd->decode_dense.lut;
+    ra.compact = 1;
+    HEC_HIP(launch_rs104_ragged(ra, true, sc->stream));
+    HEC_HIP(hipMemcpyAsync(sc->host + in_total, sc->dev + in_total, total - in_total, hipMemcpyDeviceToHost,
+                           sc->stream));
+    HEC_HIP(hipStreamSynchronize(sc->stream));
+    // hand back the erased shards
+    parallel_for(jobs.size(), total - in_total, [&](size_t j) {
+        int r = 0;
+        for (int i = 0; i < n; ++i)
+            if (!((jobs[j].mask >> i) & 1)) take(j, i, sc->host + lay[j].out_off + uint64_t(r++) * lay[j].Lp);
+    });
+    return HEC_OK;
+}
+
 }  // namespace hec
 
 using namespace hec;
@@ -79,11 +162,10 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
     // 1. validate every stripe first (upstream reconstruct checks, per stripe)
     struct Active {
         size_t s;
-        uint64_t L, Lp, off, out_off;
+        uint64_t L;
         uint32_t mask;
     };
     std::vector<Active> act;
-    uint64_t total = 0;
     for (size_t s = 0; s < n_stripes; ++s) {
         const uint8_t* pr = present + s * n;
         uint64_t L = 0;
@@ -108,16 +190,9 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
             return err;
         }
         if (np == n) continue;  // upstream no-op
-        const uint64_t Lp = (L + 15) / 16 * 16;
-        act.push_back({s, L, Lp, total, 0, mask});
-        total += (uint64_t(k) * Lp + 255) / 256 * 256;  // compact inputs: the first k present shards
+        act.push_back({s, L, mask});
     }
     if (act.empty()) return HEC_OK;
-    const uint64_t in_total = total;
-    for (Active& a : act) {  // compact outputs: the erased shards, ascending
-        a.out_off = total;
-        total += (uint64_t(n - __builtin_popcount(a.mask)) * a.Lp + 255) / 256 * 256;
-    }
 
     // Other geometries: one host-API reconstruct per stripe (same kernels, generic path).
     if (!(k == 10 && rs->m == 4)) {
@@ -132,62 +207,17 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
         return HEC_OK;
     }
 
-    GeomDevice* gd;
-    int rc = geom_device(rs, &gd);
-    if (rc) return rc;
-    RaggedScratch* sc;
-    if ((rc = ragged_scratch(&sc))) return rc;
-    std::lock_guard<std::mutex> lk(sc->mu);
-    std::vector<RaggedItem> items(act.size());
-    std::vector<uint32_t> block_item;
-    for (size_t j = 0; j < act.size(); ++j) {
-        const Active& a = act[j];
-        const uint32_t chunks = uint32_t((a.L + 4095) / 4096);
-        items[j] = RaggedItem{a.off, a.Lp, uint32_t(a.L), a.mask, uint32_t(block_item.size()), 0, a.out_off};
-        block_item.insert(block_item.end(), chunks, uint32_t(j));
-    }
-    const size_t items_bytes = items.size() * sizeof(RaggedItem);
-    const size_t meta = (items_bytes + 255) / 256 * 256 + block_item.size() * 4;
-    if ((rc = sc->reserve(total, meta))) return rc;
-    if ((rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
-    // 2. pack the survivors the decode reads (first k present shards) into slots 0..k-1
-    parallel_for(act.size(), in_total, [&](size_t j) {
-        const Active& a = act[j];
-        int used = 0;
-        for (int i = 0; i < n && used < k; ++i)
-            if ((a.mask >> i) & 1) {
-                std::memcpy(sc->host + a.off + used * a.Lp, shards[a.s * n + i], a.L);
-                ++used;
-            }
-    });
-    std::memcpy(sc->hmeta, items.data(), items_bytes);
-    const size_t map_off = (items_bytes + 255) / 256 * 256;
-    std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
-    HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, sc->stream));
-    HEC_HIP(hipMemcpyAsync(sc->dev, sc->host, in_total, hipMemcpyHostToDevice, sc->stream));
-    RaggedArgs ra{};
-    ra.base = sc->dev;
-    ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
-    ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
-    ra.n_blocks = uint32_t(block_item.size());
-    ra.tabs = gd->decode_dense.tabs;
-    ra.lut = gd->decode_dense.lut;
-    ra.compact = 1;
-    HEC_HIP(launch_rs104_ragged(ra, true, sc->stream));
-    HEC_HIP(hipMemcpyAsync(sc->host + in_total, sc->dev + in_total, total - in_total, hipMemcpyDeviceToHost,
-                           sc->stream));
-    HEC_HIP(hipStreamSynchronize(sc->stream));
-    // 3. hand back the erased shards (data shards only for reconstruct_data)
-    parallel_for(act.size(), total - in_total, [&](size_t j) {
-        const Active& a = act[j];
-        int r = 0;
-        for (int i = 0; i < n; ++i)
-            if (!((a.mask >> i) & 1)) {
-                if (!(data_only && i >= k)) std::memcpy(shards[a.s * n + i], sc->host + a.out_off + r * a.Lp, a.L);
-                ++r;
-            }
-    });
-    return HEC_OK;
+    std::vector<CompactJob> jobs(act.size());
+    for (size_t j = 0; j < act.size(); ++j) jobs[j] = CompactJob{act[j].L, act[j].mask};
+    return compact_reconstruct_104(
+        rs, jobs,
+        [&](size_t j, int, int shard, uint8_t* dst) {
+            std::memcpy(dst, shards[act[j].s * n + shard], act[j].L);
+            return HEC_OK;
+        },
+        [&](size_t j, int shard, const uint8_t* src) {
+            if (!(data_only && shard >= k)) std::memcpy(shards[act[j].s * n + shard], src, act[j].L);
+        });
 }
 
 }  // extern "C"

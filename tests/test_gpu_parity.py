@@ -126,7 +126,7 @@ def test_host_calls_staged_and_direct(gpu, staging, k, m):
             with pytest.raises(H.IncorrectShardSize):
                 rs.reconstruct([None, np.zeros(L + 1, np.uint8)] + ref[2:])
     finally:
-        H.lib.hec_set_host_staging(64 << 20)
+        H.lib.hec_set_host_staging(4 << 20)
 
 
 def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):

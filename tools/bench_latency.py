@@ -67,7 +67,7 @@ def main():
             row[mode] = {"encode_us": round(te * 1e6, 1), "reconstruct_us": round(tr * 1e6, 1),
                          "encode_GiB_s": round(10 * L / te / 2**30, 2),
                          "reconstruct_GiB_s": round(10 * L / tr / 2**30, 2), "identical": bool(ok)}
-        lib.hec_set_host_staging(64 << 20)
+        lib.hec_set_host_staging(4 << 20)
         cr = max(3, reps // 4)
         b = [f.copy() for f in full]
         t0 = time.perf_counter()

@@ -8,13 +8,14 @@
 //               (10R4W == the encode pattern with the math removed)
 // One workgroup (256 lanes x 16 B) per 4 KiB chunk unless noted.
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/membench tools/membench.hip
-// Run:   build/membench            (prints one JSON line per case)
+// Run:   build/membench [pad]      (prints one JSON line per case)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 #include <algorithm>
+#include <string>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -147,7 +148,42 @@ static void run(const char* name, const char* extra, double bytes, F f, int reps
     fflush(stdout);
 }
 
-int main() {
+// Padded layouts: 1 MiB shards at shard stride L + pad, or stripes at
+// 14 L + stripe pad (does breaking the 2^20 spacing help the write streams?).
+static int pad_sweep() {
+    const uint64_t S = 4096, L = 1ull << 20, N = 14, maxpad = 65536;
+    uint8_t* buf;
+    CHECK(hipMalloc(&buf, S * N * (L + maxpad)));
+    CHECK(hipMemset(buf, 0x5a, S * N * (L + maxpad)));
+    const uint32_t cps = uint32_t(L / 4096), grid = uint32_t(S * cps);
+    char extra[160];
+    for (uint64_t pad : {0ull, 256ull, 1024ull, 2048ull, 4096ull, 8192ull, 12288ull, 65536ull}) {
+        const uint64_t ss = L + pad;
+        snprintf(extra, sizeof extra, ", \"shard_pad\": %llu, \"stripe_pad\": 0, \"xcd_remap\": 1",
+                 (unsigned long long)pad);
+        run("10r4w", extra, double(S * 14 * L), [&] {
+            hipLaunchKernelGGL((k_nrmw<10, 4>), dim3(grid), dim3(256), 0, 0, buf, N * ss, ss, cps, 1);
+        });
+        run("0r14w", extra, double(S * 14 * L), [&] {
+            hipLaunchKernelGGL((k_nrmw<0, 14>), dim3(grid), dim3(256), 0, 0, buf, N * ss, ss, cps, 1);
+        });
+    }
+    for (uint64_t spad : {4096ull, 65536ull, 14ull * 65536ull}) {
+        snprintf(extra, sizeof extra, ", \"shard_pad\": 0, \"stripe_pad\": %llu, \"xcd_remap\": 1",
+                 (unsigned long long)spad);
+        run("10r4w", extra, double(S * 14 * L), [&] {
+            hipLaunchKernelGGL((k_nrmw<10, 4>), dim3(grid), dim3(256), 0, 0, buf, N * L + spad, L, cps, 1);
+        });
+        run("0r14w", extra, double(S * 14 * L), [&] {
+            hipLaunchKernelGGL((k_nrmw<0, 14>), dim3(grid), dim3(256), 0, 0, buf, N * L + spad, L, cps, 1);
+        });
+    }
+    CHECK(hipFree(buf));
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "pad") return pad_sweep();
     const uint64_t S = 4096, L = 1ull << 20, N = 14;
     const uint64_t total = S * N * L;  // 56 GiB
     uint8_t* buf;

@@ -39,10 +39,16 @@ __device__ __forceinline__ const __attribute__((address_space(4))) T* as_const(c
 #define HEC_NT_STORE 1
 #endif
 
+// Global-address-space views: the nontemporal hint on a flat (generic)
+// pointer is dropped by the backend (plain global_load_dwordx4), so the
+// streamed shards are accessed through address_space(1) pointers to get `nt`.
+typedef const __attribute__((address_space(1))) u32x4* gcu32x4p;
+typedef __attribute__((address_space(1))) u32x4* gu32x4p;
+
 __device__ __forceinline__ u32x4 load_full(const uint8_t* p, bool aligned) {
     if (aligned) {
 #if HEC_NT_LOAD
-        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return __builtin_nontemporal_load((gcu32x4p)(p));
 #else
         return *reinterpret_cast<const u32x4*>(p);
 #endif
@@ -55,7 +61,7 @@ __device__ __forceinline__ u32x4 load_full(const uint8_t* p, bool aligned) {
 __device__ __forceinline__ void store_full(uint8_t* p, u32x4 v, bool aligned) {
     if (aligned) {
 #if HEC_NT_STORE
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+        __builtin_nontemporal_store(v, (gu32x4p)(p));
 #else
         *reinterpret_cast<u32x4*>(p) = v;
 #endif

@@ -79,7 +79,6 @@ SIGNATURES = {
     "hec_set_kernel_mode": (_I, [_I]),
     "hec_set_host_staging": (_I, [ctypes.c_uint64]),
     "hec_set_workgroup_size": (_I, [_I]),
-    "hec_set_persistent": (_I, [_I]),
     "hec_set_xcd_parts": (_I, [_I]),
     "hec_set_chunk_rotation": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),

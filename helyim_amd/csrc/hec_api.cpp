@@ -479,12 +479,6 @@ int hec_set_workgroup_size(int threads) {
     return HEC_OK;
 }
 
-int hec_set_persistent(int wgs_per_cu) {
-    if (wgs_per_cu < 0 || wgs_per_cu > 8) return fail(HEC_ERR_INVALID_ARGUMENT, "workgroups per CU in 0..8");
-    launch_config().persist = wgs_per_cu;
-    return HEC_OK;
-}
-
 int hec_set_host_staging(uint64_t max_bytes) {
     host_staging_max() = max_bytes;
     return HEC_OK;

@@ -329,120 +329,6 @@ __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
                               a.bad_count);
 }
 
-// Persistent, software-pipelined RS(10,4) kernel (experimental launch mode,
-// speed only): `persist` workgroups per CU loop over the 4 KiB chunks with a
-// grid stride, so at any moment the whole chip works on one contiguous run of
-// chunks (few open DRAM rows), and each wave issues the 10 loads of its next
-// chunk before the GF math of the current one (memory/compute overlap at low
-// occupancy). Full chunks only (len % 4 KiB == 0, 16-byte aligned).
-struct Chunk104 {
-    const uint8_t* in;
-    uint8_t* out;
-    uint64_t o;
-    cu32p tab;
-    uint32_t in_id[10], out_id[4];
-    uint32_t nout;
-    bool live;
-};
-
-template <bool DEC>
-__device__ __forceinline__ void rs104_prepare(const ApplyArgs& a, uint64_t item, Chunk104& c) {
-    constexpr int K = 10, N = 14, R = 4;
-    const uint32_t stripe = uint32_t(item / a.chunks_per_stripe);
-    const uint32_t chunk = uint32_t(item - uint64_t(stripe) * a.chunks_per_stripe);
-    c.in = a.in_base + uint64_t(stripe) * a.in_stripe;
-    c.out = a.out_base + uint64_t(stripe) * a.out_stripe;
-    c.o = uint64_t(chunk) * (kThreads * kVecBytes) + threadIdx.x * kVecBytes;
-    c.tab = as_const(a.tabs);
-    c.nout = R;
-    c.live = true;
-    if constexpr (DEC) {
-        const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
-        const uint32_t present = __builtin_popcount(mask);
-        if (present < K || present == N) {
-            if (present < K && chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
-            c.live = false;
-            return;
-        }
-        c.nout = N - present;
-        uint32_t m = mask;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            c.in_id[i] = __builtin_ctz(m);
-            m &= m - 1;
-        }
-        uint32_t e = ~mask & ((1u << N) - 1);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            c.out_id[r] = e ? __builtin_ctz(e) : 0;
-            e &= e - 1;
-        }
-        c.tab += as_const(a.lut)[mask] * (K * R * 5);
-    } else {
-#pragma unroll
-        for (int i = 0; i < K; ++i) c.in_id[i] = i;
-#pragma unroll
-        for (int r = 0; r < R; ++r) c.out_id[r] = r;
-    }
-}
-
-__device__ __forceinline__ void rs104_issue(const Chunk104& c, uint64_t in_shard, u32x4 (&d)[10]) {
-    if (!c.live) return;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) d[i] = load_full(c.in + uint64_t(c.in_id[i]) * in_shard + c.o, true);
-}
-
-template <bool XORONLY>
-__device__ __forceinline__ void rs104_finish(const Chunk104& c, uint64_t out_shard, const u32x4 (&d)[10]) {
-    constexpr int R = 4;
-    if (!c.live) return;
-    // Opaque per chunk: keeps the loop-invariant encode tables from being
-    // hoisted out of the persistent loop into (spilled) SGPRs.
-    const uint64_t tab_bits = reinterpret_cast<uint64_t>(c.tab);
-    uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(tab_bits));
-    uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(tab_bits >> 32));
-    asm volatile("" : "+s"(lo), "+s"(hi));
-    const cu32p tab = reinterpret_cast<cu32p>((uint64_t(hi) << 32) | lo);
-    u32x4 acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 10; ++i) mac<R, XORONLY>(acc, d[i], tab + i * (R * 5));
-#pragma unroll
-    for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (r < int(c.nout)) store_full(c.out + uint64_t(c.out_id[r]) * out_shard + c.o, acc[r], true);
-}
-
-template <bool DEC, bool XORONLY>
-__global__ __launch_bounds__(kThreads) void rs104_persist_kernel(ApplyArgs a) {
-    const uint64_t total = a.n_items, G = gridDim.x;
-    uint64_t item = blockIdx.x;
-    if (item >= total) return;
-    Chunk104 c0, c1;
-    u32x4 d0[10], d1[10];
-    rs104_prepare<DEC>(a, item, c0);
-    rs104_issue(c0, a.in_shard, d0);
-    for (;;) {  // unrolled by two so the double buffer needs no register copies
-        const uint64_t n1 = item + G;
-        if (n1 < total) {
-            rs104_prepare<DEC>(a, n1, c1);
-            rs104_issue(c1, a.in_shard, d1);
-        }
-        rs104_finish<XORONLY>(c0, a.out_shard, d0);
-        if (n1 >= total) break;
-        const uint64_t n2 = n1 + G;
-        if (n2 < total) {
-            rs104_prepare<DEC>(a, n2, c0);
-            rs104_issue(c0, a.in_shard, d0);
-        }
-        rs104_finish<XORONLY>(c1, a.out_shard, d1);
-        if (n2 >= total) break;
-        item = n2;
-    }
-}
-
 // Ragged batches: every stripe has its own length, shard stride and mask
 // (degraded reads of needle intervals, mixed 64 KiB-4 MiB stripes). The host
 // lays stripes out back to back and passes a workgroup -> stripe map.
@@ -483,35 +369,10 @@ static hipError_t launch_rs104_tb(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     return hipGetLastError();
 }
 
-static int cu_count() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
-template <bool DEC, bool XORONLY>
-static hipError_t launch_rs104_persist(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(kThreads) * kVecBytes;
-    a.chunks_per_stripe = uint32_t(a.len / chunk);
-    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
-    if (a.n_items == 0) return hipSuccess;
-    uint64_t grid = uint64_t(cu_count()) * uint64_t(cfg.persist);
-    if (grid > a.n_items) grid = a.n_items;
-    hipLaunchKernelGGL((rs104_persist_kernel<DEC, XORONLY>), dim3(uint32_t(grid)), dim3(kThreads), 0, stream, a);
-    return hipGetLastError();
-}
-
 // Workgroup size (speed only): 256 threads = one 4 KiB chunk per workgroup
 // (default); 512 / 1024 give each workgroup 8 / 16 KiB contiguous per shard.
 template <bool DEC, bool XORONLY>
 static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
-    if (cfg.persist > 0 && a.len % (uint64_t(kThreads) * kVecBytes) == 0)
-        return launch_rs104_persist<DEC, XORONLY>(a, cfg, stream);
     switch (cfg.wg_threads) {
         case 512: return launch_rs104_tb<DEC, XORONLY, 512>(a, cfg, stream);
         case 1024: return launch_rs104_tb<DEC, XORONLY, 1024>(a, cfg, stream);

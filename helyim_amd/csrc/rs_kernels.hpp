@@ -84,7 +84,6 @@ struct LaunchConfig {
     int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
     int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
     int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
-    int persist = 0;             // >0: persistent pipelined RS(10,4) kernel, this many workgroups/CU
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees

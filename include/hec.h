@@ -305,11 +305,6 @@ int hec_set_kernel_mode(int mode);
 /* Workgroup size of the RS(10,4) kernel: 256 (default; one 4 KiB chunk per
  * workgroup), 512 or 1024 (8 / 16 KiB per shard per workgroup). Speed only. */
 int hec_set_workgroup_size(int threads);
-/* wgs_per_cu > 0: RS(10,4) batches whose shard length is a multiple of 4 KiB
- * run a persistent, software-pipelined kernel with this many workgroups per
- * CU (each wave loads its next chunk before the math of the current one);
- * 0 = one workgroup per chunk (default). Speed only. */
-int hec_set_persistent(int wgs_per_cu);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables

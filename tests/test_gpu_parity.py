@@ -200,37 +200,6 @@ def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc, wg):
         H.lib.hec_set_workgroup_size(256)
 
 
-@pytest.mark.parametrize("persist", [1, 2, 3])
-def test_persistent_kernel_identical(gpu, persist):
-    """The persistent pipelined RS(10,4) kernel (hec_set_persistent) gives
-    the default kernel's bytes for encode and every-mask decode."""
-    import torch
-    import helyim_amd as H
-    import helyim_amd.batch as B
-    rs = H.ReedSolomon(10, 4)
-    S, L = 301, 5 * 4096
-    t = _stripes(S, L)
-    ref = t.clone()
-    B.encode_batch(rs, ref)
-    rng = np.random.default_rng(persist)
-    pats = [c for e in range(0, 6) for c in itertools.combinations(range(14), e)]
-    masks = np.array([((1 << 14) - 1) & ~sum(1 << i for i in pats[int(j)])
-                      for j in rng.integers(0, len(pats), S)], dtype=np.int32)
-    try:
-        assert H.lib.hec_set_persistent(persist) == 0
-        B.encode_batch(rs, t)
-        torch.cuda.synchronize()
-        assert torch.equal(t, ref)
-        er = torch.from_numpy(((masks[:, None] >> np.arange(14)[None, :]) & 1) == 0).cuda()
-        t[er] = 0
-        B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
-        torch.cuda.synchronize()
-        ok = torch.from_numpy(np.array([bin(int(m)).count("1") >= 10 for m in masks])).cuda()
-        assert torch.equal(t[ok], ref[ok])
-    finally:
-        H.lib.hec_set_persistent(0)
-
-
 def test_batch_encode_separate_and_unaligned(gpu):
     import torch
     import helyim_amd as H

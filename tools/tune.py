@@ -29,7 +29,6 @@ def main():
     ap.add_argument("--parts", default="1", help="regions per XCD (xcd_remap 1)")
     ap.add_argument("--rots", default="0", help="hashed per-stripe chunk rotation (0/1)")
     ap.add_argument("--wgs", default="256", help="RS(10,4) workgroup sizes (256/512/1024)")
-    ap.add_argument("--persist", default="0", help="persistent pipelined kernel: workgroups per CU (0 = off)")
     ap.add_argument("--pad", type=int, default=0, help="extra bytes between shards (breaks 2^20 strides)")
     ap.add_argument("--tile", type=int, default=0,
                     help="interleaved layout: every shard split in tiles of this many bytes, the 14 "
@@ -54,13 +53,12 @@ def main():
     good = t[:8].clone()
     ints = lambda x: [int(y) for y in x.split(",")]
     configs = list(itertools.product(ints(args.modes), ints(args.vecs), ints(args.blocks), ints(args.remaps),
-                                     ints(args.bpcs), ints(args.parts), ints(args.rots), ints(args.wgs), ints(args.persist)))
+                                     ints(args.bpcs), ints(args.parts), ints(args.rots), ints(args.wgs)))
     res = {c: {"enc": [], "dec": []} for c in configs}
     s = torch.cuda.current_stream()
     for _ in range(args.rounds):
         for c in configs:
-            mode, v, b, rm, bpc, parts, rot, wg, pers = c
-            H.lib.hec_set_persistent(pers)
+            mode, v, b, rm, bpc, parts, rot, wg = c
             H.lib.hec_set_kernel_mode(mode)
             H.lib.hec_set_workgroup_size(wg)
             H.lib.hec_set_xcd_parts(parts)
@@ -79,14 +77,13 @@ def main():
     H.lib.hec_set_xcd_parts(1)
     H.lib.hec_set_chunk_rotation(0)
     H.lib.hec_set_workgroup_size(256)
-    H.lib.hec_set_persistent(0)
     B.set_launch_config()
     nbytes = S * 14 * L
     for c in configs:
         enc, dec = np.array(res[c]["enc"]), np.array(res[c]["dec"])
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "pad": args.pad, "tile": args.tile,
                           "mode": ["gf", "xor_ceiling"][c[0]], "vec_per_thread": c[1], "max_blocks": c[2],
-                          "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7], "persist": c[8],
+                          "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7],
                           "enc_ms_med": round(float(np.median(enc)), 3), "enc_ms_min": round(float(enc.min()), 3),
                           "enc_GBps": round(nbytes / np.median(enc) / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 3),

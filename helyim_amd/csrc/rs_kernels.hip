@@ -329,6 +329,80 @@ __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
                               a.bad_count);
 }
 
+// Two 4 KiB chunks per workgroup (launch config vec_per_thread = 2; shard
+// length a multiple of 8 KiB): each lane issues the 20 loads of both chunks,
+// then does the math of the first while the second's loads are in flight.
+// Chunks 2p and 2p+1 share a stripe, hence shard ids and tables.
+template <bool DEC, bool XORONLY>
+__global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
+    constexpr int K = 10, N = 14, R = 4, U = 2;
+    const uint32_t pair = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
+    const uint32_t pairs_per_stripe = a.chunks_per_stripe / U;
+    const uint32_t stripe = pair / pairs_per_stripe;
+    const uint32_t p = pair - stripe * pairs_per_stripe;
+    const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
+    uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
+    uint32_t in_id[K], out_id[R];
+    uint32_t nout = R;
+    cu32p tab = as_const(a.tabs);
+    if constexpr (DEC) {
+        const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
+        const uint32_t present = __builtin_popcount(mask);
+        if (present < K) {
+            if (p == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
+            return;
+        }
+        if (present == N) return;
+        nout = N - present;
+        uint32_t m = mask;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            in_id[i] = __builtin_ctz(m);
+            m &= m - 1;
+        }
+        uint32_t e = ~mask & ((1u << N) - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            out_id[r] = e ? __builtin_ctz(e) : 0;
+            e &= e - 1;
+        }
+        tab += as_const(a.lut)[mask] * (K * R * 5);
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) in_id[i] = i;
+#pragma unroll
+        for (int r = 0; r < R; ++r) out_id[r] = r;
+    }
+    const uint64_t o0 = uint64_t(p) * (U * kThreads * kVecBytes) + threadIdx.x * kVecBytes;
+    u32x4 d[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            d[u][i] = load_full(in_b + uint64_t(in_id[i]) * a.in_shard + o0 + u * (kThreads * kVecBytes), true);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        // Opaque per chunk: the table words are re-read (scalar cache hits)
+        // for the second chunk instead of held live across both (SGPR spills).
+        const uint64_t tb = reinterpret_cast<uint64_t>(tab);
+        uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(tb)), hi = __builtin_amdgcn_readfirstlane(uint32_t(tb >> 32));
+        asm volatile("" : "+s"(lo), "+s"(hi));
+        const cu32p t = reinterpret_cast<cu32p>((uint64_t(hi) << 32) | lo);
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < K; ++i) mac<R, XORONLY>(acc, d[u][i], t + i * (R * 5));
+#pragma unroll
+        for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r < int(nout))
+                store_full(out_b + uint64_t(out_id[r]) * a.out_shard + o0 + u * (kThreads * kVecBytes), acc[r],
+                           true);
+    }
+}
+
 // Ragged batches: every stripe has its own length, shard stride and mask
 // (degraded reads of needle intervals, mixed 64 KiB-4 MiB stripes). The host
 // lays stripes out back to back and passes a workgroup -> stripe map.
@@ -372,7 +446,23 @@ static hipError_t launch_rs104_tb(ApplyArgs a, const LaunchConfig& cfg, hipStrea
 // Workgroup size (speed only): 256 threads = one 4 KiB chunk per workgroup
 // (default); 512 / 1024 give each workgroup 8 / 16 KiB contiguous per shard.
 template <bool DEC, bool XORONLY>
+static hipError_t launch_rs104_pair(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
+    const uint64_t chunk = uint64_t(kThreads) * kVecBytes;
+    a.chunks_per_stripe = uint32_t(a.len / chunk);
+    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
+    if (a.n_items == 0) return hipSuccess;
+    a.xcd_remap = uint32_t(cfg.xcd_remap);
+    a.xcd_parts = uint32_t(cfg.xcd_parts);
+    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
+    hipLaunchKernelGGL((rs104_pair_kernel<DEC, XORONLY>), dim3(uint32_t(a.n_items / 2)), dim3(kThreads), lds, stream,
+                       a);
+    return hipGetLastError();
+}
+
+template <bool DEC, bool XORONLY>
 static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
+    if (cfg.vec_per_thread == 2 && a.len % (2 * uint64_t(kThreads) * kVecBytes) == 0)
+        return launch_rs104_pair<DEC, XORONLY>(a, cfg, stream);
     switch (cfg.wg_threads) {
         case 512: return launch_rs104_tb<DEC, XORONLY, 512>(a, cfg, stream);
         case 1024: return launch_rs104_tb<DEC, XORONLY, 1024>(a, cfg, stream);
@@ -400,7 +490,9 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
                         hipStream_t stream) {
     // RS(10,4) fast path: fixed 4-row table stride, one 4 KiB chunk per workgroup.
     const uint64_t items = ((a.len + 4095) / 4096) * a.n_stripes;
-    if (a.fast104 && aligned && cfg.vec_per_thread == 1 && cfg.max_blocks == 0 && items < 0x7FFFFFFFull) {
+    const bool pair_ok = cfg.vec_per_thread == 2 && a.len % 8192 == 0;
+    if (a.fast104 && aligned && (cfg.vec_per_thread == 1 || pair_ok) && cfg.max_blocks == 0 &&
+        items < 0x7FFFFFFFull) {
         if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, cfg, stream)
                                           : launch_rs104<true, false>(a, cfg, stream);
         return cfg.mode == 1 ? launch_rs104<false, true>(a, cfg, stream) : launch_rs104<false, false>(a, cfg, stream);

@@ -200,6 +200,37 @@ def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc, wg):
         H.lib.hec_set_workgroup_size(256)
 
 
+@pytest.mark.parametrize("remap,bpc", [(1, 0), (0, 2), (1, 3)])
+def test_pair_kernel_identical(gpu, remap, bpc):
+    """Two chunks per workgroup (vec_per_thread 2, shard length a multiple of
+    8 KiB) gives the default kernel's bytes for encode and every-mask decode."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = 301, 5 * 8192
+    t = _stripes(S, L)
+    ref = t.clone()
+    B.encode_batch(rs, ref)
+    rng = np.random.default_rng(remap * 10 + bpc)
+    pats = [c for e in range(0, 6) for c in itertools.combinations(range(14), e)]
+    masks = np.array([((1 << 14) - 1) & ~sum(1 << i for i in pats[int(j)])
+                      for j in rng.integers(0, len(pats), S)], dtype=np.int32)
+    try:
+        B.set_launch_config(2, 0, remap, bpc)
+        B.encode_batch(rs, t)
+        torch.cuda.synchronize()
+        assert torch.equal(t, ref)
+        er = torch.from_numpy(((masks[:, None] >> np.arange(14)[None, :]) & 1) == 0).cuda()
+        t[er] = 0
+        B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
+        torch.cuda.synchronize()
+        ok = torch.from_numpy(np.array([bin(int(m)).count("1") >= 10 for m in masks])).cuda()
+        assert torch.equal(t[ok], ref[ok])
+    finally:
+        B.set_launch_config()
+
+
 def test_batch_encode_separate_and_unaligned(gpu):
     import torch
     import helyim_amd as H

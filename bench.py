@@ -341,6 +341,10 @@ def main():
         ref = corc.encode_stripes(t[0:2, :K_DATA].cpu().numpy().copy())
         chk_ok &= bool(np.array_equal(t[0:2, K_DATA:].cpu().numpy(), ref))
     del t
+    # every rank's verification counts: the job is verified only if all are
+    chk_ok = reduce_max(0.0 if chk_ok else 1.0, world) == 0.0
+    enc_ms = reduce_max(enc_ms, world)
+    dec_ms = reduce_max(dec_ms, world)
 
     enc_bytes = S * N_TOTAL * L                      # read 10 L + write 4 L per stripe
     dec_bytes = S * (K_DATA + 4) * L                 # read 10 survivors + write 4 erased

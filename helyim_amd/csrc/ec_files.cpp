@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdio>
@@ -367,6 +368,21 @@ struct Rs104 {
     ~Rs104() { hec_rs_free(rs); }
 };
 
+// Reserve the final size of freshly created output files up front, one
+// fallocate per file on its own thread. FALLOC_FL_KEEP_SIZE leaves the visible
+// size to the writes, so a failed call leaves the bytes the reference would.
+// Speed only: the filesystem allocates each file in one call instead of page
+// by page inside the writes. Filesystems without fallocate are skipped
+// silently. HEC_NO_PREALLOC=1 turns it off (measurement).
+void preallocate(const int* fds, int n, uint64_t bytes) {
+    static const bool disabled = std::getenv("HEC_NO_PREALLOC") != nullptr;
+    if (disabled || bytes == 0) return;
+    std::vector<std::thread> th;
+    for (int i = 0; i < n; ++i)
+        if (fds[i] >= 0) th.emplace_back([fd = fds[i], bytes] { (void)::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, off_t(bytes)); });
+    for (auto& t : th) t.join();
+}
+
 // Split [off, off+len) into up to `parts` read pieces of whole `unit`s.
 void add_reads(std::vector<ReadSeg>& v, int fd, uint64_t host_off, uint64_t len, uint64_t file_off, uint64_t unit,
                int parts) {
@@ -408,6 +424,11 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     const uint64_t n_small = small_bytes > 0 ? (uint64_t(small_bytes) + small_row - 1) / small_row : 0;
     GeomDevice* gd;
     if ((rc = geom_device(rs.rs, &gd))) return rc;
+    {
+        int fds[N];
+        for (int i = 0; i < N; ++i) fds[i] = out[i].fd;
+        preallocate(fds, N, n_large * large + n_small * small);
+    }
 
     const uint64_t T = n_large ? std::min<uint64_t>(large, kLargeSlice) : 0;                    // large-row slice
     const uint64_t B = std::min(n_small, std::max<uint64_t>(1, kBatchBytes / small_row));  // small rows per job
@@ -558,6 +579,11 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
             ~PsGuard() { p.release(); }
         } pg{ps};
         if ((rc = ps.upload(hp, nullptr, nullptr))) return rc;
+        {
+            int fds[N];
+            for (int i = 0; i < N; ++i) fds[i] = has[i] ? -1 : out[i].fd;
+            preallocate(fds, N, rows * row_size);
+        }
         const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(rows, kBatchBytes / (K * row_size)));
         const uint64_t slot = B * row_size;  // bytes per shard slot: layout [14][B rows]
         PipelineLease lease;

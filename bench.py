@@ -375,7 +375,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(enc_gbps, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "kernel": "rs104_kernel<DEC=false> (encode)",
+                         "kernel": H.lib.hec_encode_kernel_name(L).decode(),
                          "algorithmic_bytes_per_launch": enc_bytes},
             "encode": {"ms_per_launch": round(enc_ms, 4), "GB_s_hbm": round(enc_gbps, 1),
                        "data_GiB_s": round(S * K_DATA * L / (enc_ms * 1e-3) / 2**30, 1)},

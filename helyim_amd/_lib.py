@@ -79,9 +79,11 @@ SIGNATURES = {
     "hec_set_kernel_mode": (_I, [_I]),
     "hec_set_host_staging": (_I, [ctypes.c_uint64]),
     "hec_set_workgroup_size": (_I, [_I]),
+    "hec_set_encode_kernel": (_I, [_I]),
     "hec_set_xcd_parts": (_I, [_I]),
     "hec_set_chunk_rotation": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
+    "hec_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -449,6 +449,8 @@ const char* hec_last_error_detail(void) { return g_detail.c_str(); }
 
 const char* hec_version(void) { return "libhec 0.1.0 (gfx950)"; }
 
+const char* hec_encode_kernel_name(uint64_t shard_len) { return encode_kernel_name(shard_len, launch_config()); }
+
 int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, int blocks_per_cu) {
     if (vec_per_thread != 1 && vec_per_thread != 2 && vec_per_thread != 4)
         return fail(HEC_ERR_INVALID_ARGUMENT, "vec_per_thread must be 1, 2 or 4");
@@ -473,9 +475,15 @@ int hec_set_chunk_rotation(int on) {
 }
 
 int hec_set_workgroup_size(int threads) {
-    if (threads != 256 && threads != 512 && threads != 1024)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "workgroup size must be 256, 512 or 1024");
+    if (threads != 128 && threads != 256 && threads != 512 && threads != 1024)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "workgroup size must be 128, 256, 512 or 1024");
     launch_config().wg_threads = threads;
+    return HEC_OK;
+}
+
+int hec_set_encode_kernel(int kind) {
+    if (kind < 0 || kind > 4) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0..4");
+    launch_config().bitslice = kind;
     return HEC_OK;
 }
 

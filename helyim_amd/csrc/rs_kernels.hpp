@@ -84,12 +84,20 @@ struct LaunchConfig {
     int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
     int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
     int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
+    int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
+                                 // bytes: 1 = bit-sliced XOR program (default), 2 = same at >= 3
+                                 // waves/SIMD, 3/4 = LDS-DMA pipelined (window / contiguous order),
+                                 // 0 = table-lookup multiply (speed only)
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees
 // (10 selects the unrolled helyim RS(10,4) path; anything else the generic loop).
 hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
                         hipStream_t stream);
+
+// Name of the kernel an aligned RS(10,4) device encode of this shard length
+// runs under cfg (introspection for benchmarks and profiles).
+const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg);
 
 // splitmix64 byte stream per stripe (bench/test data generator):
 // stripe s: bytes_per_stripe bytes at base + s*stripe_stride, word n (n>=1) =

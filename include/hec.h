@@ -302,9 +302,18 @@ int hec_set_chunk_rotation(int on);
  * loads, stores and addressing; WRONG parity by design), used only to measure
  * the achievable HBM rate of this access pattern. Returns HEC_OK. */
 int hec_set_kernel_mode(int mode);
-/* Workgroup size of the RS(10,4) kernel: 256 (default; one 4 KiB chunk per
- * workgroup), 512 or 1024 (8 / 16 KiB per shard per workgroup). Speed only. */
+/* Workgroup size of the RS(10,4) kernels: 256 (default; one 4 KiB chunk per
+ * workgroup), 512 or 1024 (8 / 16 KiB per shard per workgroup); 128 applies to
+ * the bit-sliced encode only (others use 256). Speed only. */
 int hec_set_workgroup_size(int threads);
+/* RS(10,4) encode kernel on shard lengths that are a multiple of
+ * 32 x workgroup size bytes (8 KiB at 256 threads): 1 = bit-sliced (bytes
+ * transposed into bit planes, the fixed parity matrix applied as a generated
+ * XOR program; the default), 2 = the same compiled for >= 3 waves per SIMD,
+ * 3 / 4 = the same software-pipelined through LDS-DMA (persistent grid,
+ * window / contiguous chunk order), 0 = table-lookup GF multiply. All give
+ * identical parity (parity-tested); speed only. */
+int hec_set_encode_kernel(int kind);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables
@@ -312,6 +321,9 @@ int hec_set_workgroup_size(int threads);
 int hec_set_host_staging(uint64_t max_bytes);
 /* Version string of the library build. */
 const char* hec_version(void);
+/* Name of the kernel a 16-byte-aligned RS(10,4) device batch encode of this
+ * shard length runs under the current launch configuration (static string). */
+const char* hec_encode_kernel_name(uint64_t shard_len);
 
 #ifdef __cplusplus
 }

@@ -231,6 +231,50 @@ def test_pair_kernel_identical(gpu, remap, bpc):
         B.set_launch_config()
 
 
+@pytest.mark.parametrize("kind,wg,remap,bpc", [(0, 256, 1, 0), (1, 256, 1, 0), (1, 256, 0, 2), (1, 128, 1, 3), (2, 256, 1, 0),
+                                               (2, 512, 1, 0), (3, 256, 1, 0), (3, 128, 0, 1), (4, 256, 1, 0),
+                                               (4, 128, 1, 2)])
+def test_bitslice_encode_matches_oracle(gpu, kind, wg, remap, bpc):
+    """The encode kernels (hec_set_encode_kernel 0: table lookup; 1..4 bit-sliced: plain,
+    >= 3 waves/SIMD, LDS-DMA pipelined in window / contiguous order) against
+    the C oracle: lengths that are a multiple of 32 x workgroup size take them,
+    others fall back to the table kernel; in-place [S][14][L] and separate
+    data/parity buffers."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    try:
+        assert H.lib.hec_set_encode_kernel(kind) == 0
+        assert H.lib.hec_set_workgroup_size(wg) == 0
+        B.set_launch_config(1, 0, remap, bpc)
+        for S, L in ((5, 8192), (3, 3 * 8192), (2, 1 << 20), (4, 8192 + 16), (3, 4096), (700, 16384)):
+            t = _stripes(S, L)
+            B.encode_batch(rs, t)
+            torch.cuda.synchronize()
+            host = t.cpu().numpy()
+            ref = corc.encode_stripes(np.ascontiguousarray(host[:, :10]))
+            assert np.array_equal(host[:, 10:], ref), (S, L)
+            data = t[:, :10].contiguous()
+            par = torch.zeros((S, 4, L), dtype=torch.uint8, device="cuda")
+            B.encode_batch_sep(rs, data, par)
+            torch.cuda.synchronize()
+            assert np.array_equal(par.cpu().numpy(), ref), (S, L)
+        # every byte value in every shard position (all 256 x 10 inputs)
+        S, L = 10, 8192
+        t = torch.zeros((S, 14, L), dtype=torch.uint8, device="cuda")
+        for s in range(S):
+            t[s, s] = torch.arange(L, device="cuda").to(torch.uint8)
+        B.encode_batch(rs, t)
+        torch.cuda.synchronize()
+        host = t.cpu().numpy()
+        assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
+    finally:
+        H.lib.hec_set_encode_kernel(1)
+        H.lib.hec_set_workgroup_size(256)
+        B.set_launch_config()
+
+
 def test_batch_encode_separate_and_unaligned(gpu):
     import torch
     import helyim_amd as H

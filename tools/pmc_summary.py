@@ -18,24 +18,30 @@ import sys
 
 
 def load(path, counter):
-    """-> {kernel name: [bytes per full-grid dispatch, ...]}"""
+    """-> ({kernel name: [bytes per full-size dispatch, ...]}, {kernel: grid})
+    keeping, per kernel, only its largest-grid dispatches (the BASELINE batch;
+    the bench's small verification launches are dropped)."""
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
-    full = max(int(r["Grid_Size"]) for r in rows)
-    rows = [r for r in rows if int(r["Grid_Size"]) == full]
+    grids = {}
+    for r in rows:
+        grids[r["Kernel_Name"]] = max(grids.get(r["Kernel_Name"], 0), int(r["Grid_Size"]))
+    rows = [r for r in rows if int(r["Grid_Size"]) == grids[r["Kernel_Name"]]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     out = {}
     for r in rows:
         out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]) * 1024)
-    return out, full
+    return out, grids
 
 
 def split(per_kernel):
-    """encode / decode series: rs104_kernel<false,...> / <true,...>; a single
-    generic kernel alternates encode (even) / decode (odd)."""
-    enc = [v for k, v in per_kernel.items() if "rs104_kernel<false" in k]
-    dec = [v for k, v in per_kernel.items() if "rs104_kernel<true" in k]
+    """encode / decode series by kernel name: the encode kernel is
+    rs104_bs_encode_kernel (bit-sliced) or rs104_kernel<false, ...>, decode is
+    rs104_kernel<true, ...>; a single generic kernel alternates encode (even)
+    / decode (odd)."""
+    enc = [k for k in per_kernel if "rs104_bs_encode_kernel" in k or "rs104_kernel<false" in k]
+    dec = [k for k in per_kernel if "rs104_kernel<true" in k]
     if enc and dec:
-        return enc[0], dec[0], sorted(per_kernel)
+        return per_kernel[enc[0]], per_kernel[dec[0]], [enc[0], dec[0]]
     (k, v), = per_kernel.items()
     return v[0::2], v[1::2], [k]
 
@@ -54,7 +60,7 @@ def main():
     out = {
         "source": src,
         "kernel": kname,
-        "grid_size_threads": grid,
+        "grid_size_threads": {k: grid[k] for k in kname},
         "workload": f"{S} stripes x {L} B, RS(10,4)",
         "correction": "FETCH_SIZE*1024*2 (gfx950 half-count on 16B/lane streams), WRITE_SIZE*1024",
         "encode_hbm_read_bytes_per_launch": enc_r,

@@ -113,6 +113,42 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R], const u32x4 d, const __a
 
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
+// Two inputs at once: the six lookups of a row are folded into the
+// accumulator by three 3-input XORs (v_bitop3) instead of four ops.
+template <int R>
+__device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R], const u32x4 d0, const u32x4 d1, cu32p tab0, cu32p tab1) {
+    uint32_t s[2][3][4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t x0 = d0[w], x1 = d1[w];
+        s[0][0][w] = x0 & 0x07070707u;
+        s[0][1][w] = (x0 >> 3) & 0x07070707u;
+        s[0][2][w] = (x0 >> 6) & 0x03030303u;
+        s[1][0][w] = x1 & 0x07070707u;
+        s[1][1][w] = (x1 >> 3) & 0x07070707u;
+        s[1][2][w] = (x1 >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t a0l = tab0[r * 5 + 0], a0h = tab0[r * 5 + 1], a1l = tab0[r * 5 + 2], a1h = tab0[r * 5 + 3],
+                       a2 = tab0[r * 5 + 4];
+        const uint32_t b0l = tab1[r * 5 + 0], b0h = tab1[r * 5 + 1], b1l = tab1[r * 5 + 2], b1h = tab1[r * 5 + 3],
+                       b2 = tab1[r * 5 + 4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t p0 = __builtin_amdgcn_perm(a0h, a0l, s[0][0][w]);
+            const uint32_t p1 = __builtin_amdgcn_perm(a1h, a1l, s[0][1][w]);
+            const uint32_t p2 = __builtin_amdgcn_perm(a2, a2, s[0][2][w]);
+            const uint32_t q0 = __builtin_amdgcn_perm(b0h, b0l, s[1][0][w]);
+            const uint32_t q1 = __builtin_amdgcn_perm(b1h, b1l, s[1][1][w]);
+            const uint32_t q2 = __builtin_amdgcn_perm(b2, b2, s[1][2][w]);
+            uint32_t x = __builtin_amdgcn_bitop3_b32(acc[r][w], p0, p1, 0x96);
+            x = __builtin_amdgcn_bitop3_b32(x, p2, q0, 0x96);
+            acc[r][w] = __builtin_amdgcn_bitop3_b32(x, q1, q2, 0x96);
+        }
+    }
+}
+
 // Diagnostic bandwidth ceiling: same loads/stores/addressing, GF math replaced
 // by a plain XOR (wrong parity by design; never used by the product paths).
 template <int R, bool XORONLY>
@@ -293,8 +329,13 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
         u32x4 d[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) d[i] = load_full(in_b + uint64_t(in_id[i]) * in_shard + o, true);
+        if constexpr (XORONLY) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) mac<R, XORONLY>(acc, d[i], tab + i * (R * 5));
+            for (int i = 0; i < K; ++i) mac<R, true>(acc, d[i], tab + i * (R * 5));
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; i += 2) gf_mac2<R>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5));
+        }
         // Materialise every row before the uniform `r < nout` store branches:
         // otherwise the compiler sinks each row's math into its branch, keeps
         // all 200 table words live and spills SGPRs (154 VGPRs, 3 waves/SIMD).

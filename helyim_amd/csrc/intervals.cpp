@@ -236,6 +236,10 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     std::vector<RaggedItem> items;
     std::vector<uint32_t> block_item;
     items.reserve(n);
+    // encode of lengths that are all multiples of 8 KiB: the bit-sliced kernel
+    bool bitslice = !decode && launch_config().bitslice != 0 && launch_config().mode == 0;
+    for (uint32_t j = 0; j < n && bitslice; ++j) bitslice = descs[j].shard_len % kBsChunk == 0;
+    const uint32_t chunk_bytes = bitslice ? kBsChunk : 4096;
     for (uint32_t j = 0; j < n; ++j) {
         const hec_stripe_desc& d = descs[j];
         if (d.shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "stripe " + std::to_string(j));
@@ -243,7 +247,7 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
             d.shard_stride < d.shard_len)
             return fail(HEC_ERR_INVALID_ARGUMENT, "stripe " + std::to_string(j) +
                                                       ": offset/stride must be 16-byte aligned, stride >= len");
-        const uint32_t chunks = (d.shard_len + 4095) / 4096;
+        const uint32_t chunks = (d.shard_len + chunk_bytes - 1) / chunk_bytes;
         items.push_back(RaggedItem{d.offset, d.shard_stride, d.shard_len, d.present_mask,
                                    uint32_t(block_item.size()), 0, 0});
         block_item.insert(block_item.end(), chunks, j);
@@ -273,7 +277,10 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     ra.tabs = decode ? gd->decode_dense.tabs : gd->encode.tabs;
     ra.lut = decode ? gd->decode_dense.lut : nullptr;
     ra.bad_count = d_bad;
-    HEC_HIP(launch_rs104_ragged(ra, decode, stream));
+    if (bitslice)
+        HEC_HIP(launch_rs104_bs_ragged(ra, stream));
+    else
+        HEC_HIP(launch_rs104_ragged(ra, decode, stream));
     HEC_HIP(hipEventRecord(sc->meta_free, stream));
     return HEC_OK;
 }

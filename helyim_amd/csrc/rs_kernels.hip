@@ -482,21 +482,19 @@ __device__ __forceinline__ void transpose8(uint32_t* r) {
     for (int i = 0; i < 8; i += 2) swap_blocks<1, 0x55555555u>(r[i], r[i + 1]);
 }
 
-template <int TB, int MINW>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MINW))) void rs104_bs_encode_kernel(ApplyArgs a) {
+// One 2*TB*16-byte column range (`chunk`) of one stripe: inputs 0..9 at in_b,
+// parity 0..3 at out_b.
+template <int TB>
+__device__ __forceinline__ void rs104_bs_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
+                                               uint64_t out_shard, uint32_t chunk) {
     constexpr int K = 10, R = 4;
-    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
-    const uint32_t stripe = item / a.chunks_per_stripe;
-    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
-    const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
-    uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
     const uint64_t o0 = uint64_t(chunk) * (TB * 2 * kVecBytes) + threadIdx.x * kVecBytes;
     const uint64_t o1 = o0 + TB * kVecBytes;
     u32x4 d[K][2];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        d[i][0] = load_full(in_b + uint64_t(i) * a.in_shard + o0, true);
-        d[i][1] = load_full(in_b + uint64_t(i) * a.in_shard + o1, true);
+        d[i][0] = load_full(in_b + uint64_t(i) * in_shard + o0, true);
+        d[i][1] = load_full(in_b + uint64_t(i) * in_shard + o1, true);
     }
     uint32_t p[K * 8];
 #pragma unroll
@@ -513,11 +511,37 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MINW))) void
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         transpose8(q + 8 * j);
-        store_full(out_b + uint64_t(j) * a.out_shard + o0, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]},
+        store_full(out_b + uint64_t(j) * out_shard + o0, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]},
                    true);
-        store_full(out_b + uint64_t(j) * a.out_shard + o1,
+        store_full(out_b + uint64_t(j) * out_shard + o1,
                    u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]}, true);
     }
+}
+
+template <int TB, int MINW>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MINW))) void rs104_bs_encode_kernel(ApplyArgs a) {
+    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
+    const uint32_t stripe = item / a.chunks_per_stripe;
+    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
+    rs104_bs_chunk<TB>(a.in_base + uint64_t(stripe) * a.in_stripe, a.out_base + uint64_t(stripe) * a.out_stripe,
+                       a.in_shard, a.out_shard, chunk);
+}
+
+// Ragged encode with every stripe length a multiple of 8 KiB: workgroup ->
+// stripe map as rs104_ragged_kernel, one 8 KiB column range per workgroup.
+__global__ __launch_bounds__(kThreads) void rs104_bs_ragged_kernel(RaggedArgs a) {
+    const uint32_t s = as_const(a.block_item)[blockIdx.x];
+    const __attribute__((address_space(4))) RaggedItem* it = as_const(a.items) + s;
+    const uint64_t off = it->off, stride = it->shard_stride;
+    const uint32_t first = it->first_block;
+    const uint8_t* b = a.base + off;
+    rs104_bs_chunk<kThreads>(b, a.base + off + 10 * stride, stride, stride, blockIdx.x - first);
+}
+
+hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
+    if (a.n_blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(rs104_bs_ragged_kernel, dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
 }
 
 template <int TB, int MINW>

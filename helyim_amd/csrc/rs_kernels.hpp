@@ -74,6 +74,10 @@ struct RaggedArgs {
 };
 
 hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream);
+// Bit-sliced ragged encode: every stripe's length a multiple of kBsChunk bytes;
+// the workgroup map has len / kBsChunk entries per stripe.
+constexpr uint32_t kBsChunk = 2 * kThreads * kVecBytes;  // 8 KiB
+hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream);
 
 struct LaunchConfig {
     int vec_per_thread = 1;      // 16-byte vectors per lane per chunk (1, 2 or 4)

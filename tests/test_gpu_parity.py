@@ -367,16 +367,21 @@ def test_full_config_roundtrip(gpu):
     assert t[:, 10:].view(torch.int64).sum(dtype=torch.int64).item() == parity_sum
 
 
-def test_ragged_device_batch(gpu):
+@pytest.mark.parametrize("lengths", ["odd", "multiple_of_8k"])
+def test_ragged_device_batch(gpu, lengths):
     """Mixed-length stripes (config 5 shape plus odd lengths) in one launch each
-    for encode and reconstruct, against the C oracle."""
+    for encode and reconstruct, against the C oracle. All lengths multiples of
+    8 KiB: the encode takes the bit-sliced ragged kernel."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rs = H.ReedSolomon(10, 4)
     rng = np.random.default_rng(21)
-    lens = [1, 17, 1000, 4096, 4097, 65536, 100003, 1 << 20, 3 << 20] + \
-        [int(64 << 10) << int(rng.integers(0, 7)) for _ in range(20)]
+    lens = [int(64 << 10) << int(rng.integers(0, 7)) for _ in range(20)]
+    if lengths == "odd":
+        lens = [1, 17, 1000, 4096, 4097, 65536, 100003, 1 << 20, 3 << 20] + lens
+    else:
+        lens = [8192, 24576, 1 << 20] + lens
     descs, off = [], 0
     for L in lens:
         stride = (L + 255) // 256 * 256

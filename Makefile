@@ -4,7 +4,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 SRC := $(wildcard helyim_amd/csrc/*.cpp) $(wildcard helyim_amd/csrc/*.hip)
-HDR := $(wildcard helyim_amd/csrc/*.hpp) include/hec.h
+HDR := $(wildcard helyim_amd/csrc/*.hpp) $(wildcard helyim_amd/csrc/*.inc) include/hec.h
 OBJ := $(patsubst helyim_amd/csrc/%,build/obj/%.o,$(SRC))
 
 all: helyim_amd/libhec.so oracle

@@ -18,6 +18,7 @@
 //    data is vector traffic: coalesced 16 B/lane loads and stores (1 KiB per
 //    wave instruction), non-temporal since every byte is touched once.
 #include "rs_kernels.hpp"
+#include "bitslice.hpp"
 
 namespace hec {
 
@@ -454,34 +455,6 @@ __global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
 // dword that is ~12.5 VALU ops against ~27 for the table-lookup multiply, so
 // the math hides at lower occupancy.
 // ---------------------------------------------------------------------------
-#include "rs104_bitslice.inc"
-
-// Swap the off-diagonal s x s blocks of the 8x8 bit matrices (one per byte
-// lane) held in rows a (low) and b (high): two shifts and two bit-selects.
-template <int S, uint32_t M>
-__device__ __forceinline__ void swap_blocks(uint32_t& a, uint32_t& b) {
-    // bitop3 0xCA = S0 ? S1 : S2 per bit (an intrinsic, so the stages are not
-    // re-associated into extra ands)
-    const uint32_t na = __builtin_amdgcn_bitop3_b32(M, a, b << S, 0xCA);
-    const uint32_t nb = __builtin_amdgcn_bitop3_b32(M, a >> S, b, 0xCA);
-    a = na;
-    b = nb;
-}
-
-// In-place 8x8 bit transpose of every byte lane: afterwards r[k] bit (8L+i)
-// is bit k of byte L of the original r[i]. An involution.
-__device__ __forceinline__ void transpose8(uint32_t* r) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) swap_blocks<4, 0x0F0F0F0Fu>(r[i], r[i + 4]);
-#pragma unroll
-    for (int i = 0; i < 8; i += 4) {
-        swap_blocks<2, 0x33333333u>(r[i], r[i + 2]);
-        swap_blocks<2, 0x33333333u>(r[i + 1], r[i + 3]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i += 2) swap_blocks<1, 0x55555555u>(r[i], r[i + 1]);
-}
-
 // One 2*TB*16-byte column range (`chunk`) of one stripe: inputs 0..9 at in_b,
 // parity 0..3 at out_b.
 template <int TB>

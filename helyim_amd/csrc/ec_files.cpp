@@ -27,8 +27,10 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <future>
 #include <map>
 #include <string>
+#include <chrono>
 #include <thread>
 
 #include "hec_internal.hpp"
@@ -195,6 +197,7 @@ struct Job {
     std::vector<Copy> h2d, d2h;
     std::function<int(uint8_t* dev, hipStream_t)> kernel;
     std::vector<WriteSeg> writes;
+    std::shared_future<void> write_gate;  // optional: writes start once it is ready
 };
 
 struct Slot {
@@ -203,6 +206,17 @@ struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     bool busy = false;
+};
+
+// Stage timing of the pipeline (HEC_FILE_TRACE=1: printed to stderr at each
+// drain). Measurement only.
+struct StageClock {
+    std::atomic<int64_t> read_ns{0}, slot_wait_ns{0}, gpu_wait_ns{0}, write_ns{0}, submit_ns{0};
+    static int64_t now() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void reset() { read_ns = slot_wait_ns = gpu_wait_ns = write_ns = submit_ns = 0; }
 };
 
 // Persistent per-device pipeline (one per GPU, reused by every file call so
@@ -239,12 +253,15 @@ class FilePipeline {
         if (err_.failed()) return;
         const int si = int(next_++ % kSlots);
         Slot& s = slots_[si];
+        int64_t t0 = StageClock::now();
         {
             std::unique_lock<std::mutex> lk(mu_);
             cv_.wait(lk, [&] { return !s.busy; });
             s.busy = true;
             ++inflight_;
         }
+        int64_t t1 = StageClock::now();
+        clk_.slot_wait_ns += t1 - t0;
         if (err_.failed()) return release(si);
         // reads in parallel pieces
         std::vector<std::function<void()>> tasks;
@@ -253,8 +270,11 @@ class FilePipeline {
                 if (!err_.failed()) pread_zero(r.fd, s.host + r.host_off, r.len, r.file_off, err_);
             });
         pool_.run_all(tasks);
+        int64_t t2 = StageClock::now();
+        clk_.read_ns += t2 - t1;
         if (err_.failed()) return release(si);
         int rc = gpu(s, job);
+        clk_.submit_ns += StageClock::now() - t2;
         if (rc) {
             err_.set(rc, hec_last_error_detail());
             return release(si);
@@ -271,6 +291,13 @@ class FilePipeline {
             std::unique_lock<std::mutex> lk(mu_);
             cv_.wait(lk, [this] { return inflight_ == 0; });
         }
+        static const bool trace = std::getenv("HEC_FILE_TRACE") != nullptr;
+        if (trace)
+            std::fprintf(stderr, "hec file pipeline: slot_wait %.3f s, read %.3f s, gpu_submit %.3f s, "
+                                 "gpu_wait %.3f s, write %.3f s\n",
+                         clk_.slot_wait_ns * 1e-9, clk_.read_ns * 1e-9, clk_.submit_ns * 1e-9,
+                         clk_.gpu_wait_ns * 1e-9, clk_.write_ns * 1e-9);
+        clk_.reset();
         int code = err_.code.load();
         std::string detail = err_.detail;
         err_.code.store(HEC_OK);
@@ -307,8 +334,12 @@ class FilePipeline {
                 wq_.pop_front();
             }
             Slot& s = slots_[w.first];
+            const int64_t t0 = StageClock::now();
             hipError_t he = hipEventSynchronize(s.done);
+            const int64_t t1 = StageClock::now();
+            clk_.gpu_wait_ns += t1 - t0;
             if (he != hipSuccess) err_.set(HEC_ERR_HIP, std::string("hipEventSynchronize: ") + hipGetErrorString(he));
+            if (w.second.write_gate.valid()) w.second.write_gate.wait();
             if (!err_.failed()) {
                 std::vector<std::function<void()>> tasks;
                 for (const WriteSeg& ws : w.second.writes)
@@ -320,6 +351,7 @@ class FilePipeline {
                     });
                 pool_.run_all(tasks);
             }
+            clk_.write_ns += StageClock::now() - t1;
             release(w.first);
         }
     }
@@ -335,6 +367,7 @@ class FilePipeline {
     uint64_t next_ = 0;
     int dev_id_ = 0;
     ErrorSlot err_;
+    StageClock clk_;
 };
 
 // One pipeline per device, created on first use and intentionally never
@@ -368,19 +401,46 @@ struct Rs104 {
     ~Rs104() { hec_rs_free(rs); }
 };
 
-// Reserve the final size of freshly created output files up front, one
-// fallocate per file on its own thread. FALLOC_FL_KEEP_SIZE leaves the visible
-// size to the writes, so a failed call leaves the bytes the reference would.
-// Speed only: the filesystem allocates each file in one call instead of page
-// by page inside the writes. Filesystems without fallocate are skipped
+// Reserve the final size of freshly created output files, one fallocate per
+// file on its own thread, while the first jobs are read and coded: the
+// returned future gates the pipeline's writes. FALLOC_FL_KEEP_SIZE leaves the
+// visible size to the writes, so a failed call leaves the bytes the reference
+// would. Speed only: the filesystem allocates each file in one call instead of
+// page by page inside the writes. Filesystems without fallocate are skipped
 // silently. HEC_NO_PREALLOC=1 turns it off (measurement).
-void preallocate(const int* fds, int n, uint64_t bytes) {
+std::shared_future<void> preallocate_async(const int* fds, int n, uint64_t bytes) {
     static const bool disabled = std::getenv("HEC_NO_PREALLOC") != nullptr;
-    if (disabled || bytes == 0) return;
-    std::vector<std::thread> th;
+    if (disabled || bytes == 0) return {};
+    std::vector<int> v;
     for (int i = 0; i < n; ++i)
-        if (fds[i] >= 0) th.emplace_back([fd = fds[i], bytes] { (void)::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, off_t(bytes)); });
+        if (fds[i] >= 0) v.push_back(fds[i]);
+    return std::async(std::launch::async, [v, bytes] {
+               std::vector<std::thread> th;
+               for (int fd : v) th.emplace_back([fd, bytes] { (void)::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, off_t(bytes)); });
+               for (auto& t : th) t.join();
+           }).share();
+}
+
+// Open (create + truncate) the output files in parallel: truncating an
+// existing multi-GiB shard file frees its pages, which is slow one file at a
+// time. Same files and flags as the reference's sequential opens; on failure
+// the lowest-numbered failing file is reported.
+int open_outputs(const std::string& base, const bool* which, Fd* out) {
+    std::vector<std::thread> th;
+    int err[N];
+    for (int i = 0; i < N; ++i) {
+        err[i] = 0;
+        if (which[i])
+            th.emplace_back([&, i] {
+                out[i].fd = ::open(shard_name(base, i).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+                if (out[i].fd < 0) err[i] = errno;
+            });
+    }
     for (auto& t : th) t.join();
+    for (int i = 0; i < N; ++i)
+        if (which[i] && out[i].fd < 0)
+            return fail(HEC_ERR_IO, "open " + shard_name(base, i) + ": " + std::strerror(err[i]));
+    return HEC_OK;
 }
 
 // Split [off, off+len) into up to `parts` read pieces of whole `unit`s.
@@ -408,9 +468,10 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     if (buf_size == 0) return fail(HEC_ERR_INVALID_ARGUMENT, "zero buffer size");
 
     Fd out[N];  // open_ec_files(base, false): create + truncate (encoder.rs:111-127)
-    for (int i = 0; i < N; ++i) {
-        out[i].fd = ::open(shard_name(base, i).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        if (out[i].fd < 0) return fail(HEC_ERR_IO, "open " + shard_name(base, i) + ": " + std::strerror(errno));
+    {
+        bool all[N];
+        std::fill(all, all + N, true);
+        if ((rc = open_outputs(base, all, out))) return rc;
     }
     const uint64_t large_row = large * K, small_row = small * K;
     // the reference checks block % buf at the first row of each kind (encoder.rs:139-144)
@@ -424,10 +485,11 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     const uint64_t n_small = small_bytes > 0 ? (uint64_t(small_bytes) + small_row - 1) / small_row : 0;
     GeomDevice* gd;
     if ((rc = geom_device(rs.rs, &gd))) return rc;
+    std::shared_future<void> prealloc;
     {
         int fds[N];
         for (int i = 0; i < N; ++i) fds[i] = out[i].fd;
-        preallocate(fds, N, n_large * large + n_small * small);
+        prealloc = preallocate_async(fds, N, n_large * large + n_small * small);
     }
 
     const uint64_t T = n_large ? std::min<uint64_t>(large, kLargeSlice) : 0;                    // large-row slice
@@ -456,6 +518,7 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
             job.d2h.push_back({data_cap, data_cap, n * M});
             for (int j = 0; j < K; ++j) job.writes.push_back({out[j].fd, out_off + t, {{j * n, n}}});
             for (int j = 0; j < M; ++j) job.writes.push_back({out[K + j].fd, out_off + t, {{data_cap + j * n, n}}});
+            job.write_gate = prealloc;
             pipe.submit(std::move(job));
         }
         out_off += large;
@@ -488,6 +551,7 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
             job.writes.push_back(std::move(ws));
         }
         for (int j = 0; j < M; ++j) job.writes.push_back({out[K + j].fd, out_off, {{data_cap + j * b * small, b * small}}});
+        job.write_gate = prealloc;
         pipe.submit(std::move(job));
         out_off += b * small;
         processed += b * small_row;
@@ -579,10 +643,11 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
             ~PsGuard() { p.release(); }
         } pg{ps};
         if ((rc = ps.upload(hp, nullptr, nullptr))) return rc;
+        std::shared_future<void> prealloc;
         {
             int fds[N];
             for (int i = 0; i < N; ++i) fds[i] = has[i] ? -1 : out[i].fd;
-            preallocate(fds, N, rows * row_size);
+            prealloc = preallocate_async(fds, N, rows * row_size);
         }
         const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(rows, kBatchBytes / (K * row_size)));
         const uint64_t slot = B * row_size;  // bytes per shard slot: layout [14][B rows]
@@ -606,6 +671,7 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
                 job.d2h.push_back({id * slot, id * slot, nr * row_size});
                 job.writes.push_back({out[id].fd, off, {{id * slot, nr * row_size}}});
             }
+            job.write_gate = prealloc;
             pipe.submit(std::move(job));
         }
         if ((rc = pipe.drain())) return rc;

@@ -1,0 +1,50 @@
+"""Stage timing of the GPU file layer (write_ec_files / rebuild_ec_files) on a
+synthetic volume in /dev/shm: run with HEC_FILE_TRACE=1 to get the pipeline's
+per-stage seconds on stderr. Measurement only.
+
+python tools/file_stages.py [--gib 12] [--reps 2]
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=12.0)
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+    import helyim_amd as H
+    from tools.bench_files import make_volume
+    d = tempfile.mkdtemp(prefix="hec_stages_", dir="/dev/shm")
+    try:
+        base = os.path.join(d, "v")
+        nbytes = int(args.gib * 2**30)
+        make_volume(base + ".dat", nbytes)
+        out = {"dat_bytes": nbytes, "encode_s": [], "rebuild_s": []}
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            H.write_ec_files(base)
+            out["encode_s"].append(round(time.perf_counter() - t0, 4))
+        for _ in range(args.reps):
+            for i in (0, 5, 10, 13):
+                os.remove(base + H.to_ext(i))
+            t0 = time.perf_counter()
+            H.rebuild_ec_files(base)
+            out["rebuild_s"].append(round(time.perf_counter() - t0, 4))
+        out["encode_GiB_s"] = round(args.gib / min(out["encode_s"]), 3)
+        out["rebuild_GiB_s"] = round(args.gib / min(out["rebuild_s"]), 3)
+        print(json.dumps(out), flush=True)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

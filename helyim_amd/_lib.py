@@ -75,6 +75,15 @@ SIGNATURES = {
     "hec_read_ec_needle": (_I, [ctypes.c_char_p, _U64, _P, _S, ctypes.POINTER(_S)]),
     "hec_read_ec_needle_ex": (_I, [ctypes.c_char_p, _U64, _U64, _U64, _P, _S, ctypes.POINTER(_S)]),
     "hec_read_ec_needles": (_I, [ctypes.c_char_p, _U64, _U64, _P, _S, _P, _S, _P, _P]),
+    "hec_ec_volume_open": (_I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "hec_ec_volume_open_ex": (_I, [ctypes.c_char_p, _U64, _U64, ctypes.POINTER(_P)]),
+    "hec_ec_volume_close": (None, [_P]),
+    "hec_ec_volume_version": (_U32, [_P]),
+    "hec_ec_volume_shard_bits": (_U32, [_P]),
+    "hec_ec_volume_find_needle": (_I, [_P, _U64, ctypes.POINTER(_U32), ctypes.POINTER(ctypes.c_int32)]),
+    "hec_ec_volume_delete_needle": (_I, [_P, _U64]),
+    "hec_ec_volume_read_needle": (_I, [_P, _U64, _P, _S, ctypes.POINTER(_S)]),
+    "hec_ec_volume_read_needles": (_I, [_P, _P, _S, _P, _S, _P, _P]),
     "hec_set_launch_config": (_I, [_I, ctypes.c_long, _I, _I]),
     "hec_set_kernel_mode": (_I, [_I]),
     "hec_set_host_staging": (_I, [ctypes.c_uint64]),

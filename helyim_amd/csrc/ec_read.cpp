@@ -17,8 +17,10 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <memory>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -158,17 +160,18 @@ struct Ecx {
     ~Ecx() {
         if (fd >= 0) ::close(fd);
     }
-    int open(const std::string& base) {
+    int open(const std::string& base, bool writable = false) {
         name = base + ".ecx";
-        fd = ::open(name.c_str(), O_RDONLY);
+        fd = ::open(name.c_str(), writable ? O_RDWR : O_RDONLY);
         if (fd < 0) return io("open " + name);
         struct stat st;
         if (::fstat(fd, &st) != 0) return io("stat " + name);
         n = uint64_t(st.st_size) / kEntry;
         return HEC_OK;
     }
-    // HEC_OK with the stored offset/size, -1 when absent, or an I/O status
-    int find(uint64_t id, uint32_t* offset, int32_t* size) const {
+    // HEC_OK with the stored offset/size, -1 when absent, or an I/O status;
+    // *entry = the matching entry's index
+    int find(uint64_t id, uint32_t* offset, int32_t* size, uint64_t* entry = nullptr) const {
         uint64_t lo = 0, hi = n;
         uint8_t e[kEntry];
         while (lo < hi) {
@@ -180,6 +183,7 @@ struct Ecx {
             if (key == id) {
                 *offset = be32(e + 8);
                 *size = int32_t(be32(e + 12));
+                if (entry) *entry = mid;
                 return HEC_OK;
             }
             if (key < id)
@@ -210,11 +214,9 @@ const hec_rs* rs104() {
 // read_ec_shard_intervals over a list of (offset, size) ranges of the volume's
 // data: ranges are located, local intervals pread, lost ones rebuilt in one
 // batch. out receives the ranges' bytes back to back.
-int read_ranges(const std::string& base, uint64_t large, uint64_t small, const uint64_t* offsets,
+int read_ranges(const std::string& base, const Shards& sh, uint64_t large, uint64_t small, const uint64_t* offsets,
                 const uint64_t* sizes, size_t n, uint8_t* out) {
-    Shards sh;
-    int rc = sh.open(base);
-    if (rc) return rc;
+    int rc;
     const int f = sh.first();
     if (f < 0) return fail(HEC_ERR_SHARD_NOT_FOUND, "no .ecNN shard file for " + base);
     const uint64_t data_size = sh.size[f] * kDataShards;  // volume/mod.rs:146
@@ -274,10 +276,137 @@ int read_ranges(const std::string& base, uint64_t large, uint64_t small, const u
         });
 }
 
+int read_ranges(const std::string& base, uint64_t large, uint64_t small, const uint64_t* offsets,
+                const uint64_t* sizes, size_t n, uint8_t* out) {
+    Shards sh;
+    int rc = sh.open(base);
+    if (rc) return rc;
+    return read_ranges(base, sh, large, small, offsets, sizes, n, out);
+}
+
+// read_ec_shard_needle's data path for one needle (erasure_coding/mod.rs:129-171)
+int read_needle(const std::string& base, const Ecx& ecx, const Shards& sh, uint64_t large, uint64_t small,
+                uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out) {
+    *n_out = 0;
+    uint32_t off;
+    int32_t sz;
+    int rc = ecx.find(needle_id, &off, &sz);
+    if (rc < 0) return fail(HEC_ERR_IO, "Needle " + std::to_string(needle_id) + " is not found");
+    if (rc) return rc;
+    if (sz < 0)  // Size::is_deleted
+        return fail(HEC_ERR_NEEDLE_NOT_FOUND, "Needle " + std::to_string(needle_id) + " not found");
+    const uint64_t a_off = actual_offset(off), a_size = actual_size(sz);
+    *n_out = size_t(a_size);
+    if (a_size > cap)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "needle needs " + std::to_string(a_size) + " bytes, cap " +
+                                                  std::to_string(cap));
+    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
+    return read_ranges(base, sh, large, small, &a_off, &a_size, 1, out);
+}
+
+// Many needles: lookups, then every range in one read_ranges (one GPU batch).
+int read_needles(const std::string& base, const Ecx& ecx, const Shards& sh, uint64_t large, uint64_t small,
+                 const uint64_t* needle_ids, size_t n, uint8_t* out, size_t cap, uint64_t* out_offsets,
+                 int* statuses) {
+    std::vector<uint64_t> offs, sizes;
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t off;
+        int32_t sz;
+        out_offsets[i] = total;
+        int rc = ecx.find(needle_ids[i], &off, &sz);
+        if (rc > 0) return rc;  // I/O error on .ecx
+        if (rc < 0) {
+            statuses[i] = HEC_ERR_IO;  // not in .ecx (io::ErrorKind::NotFound)
+            continue;
+        }
+        if (sz < 0) {
+            statuses[i] = HEC_ERR_NEEDLE_NOT_FOUND;
+            continue;
+        }
+        statuses[i] = HEC_OK;
+        offs.push_back(actual_offset(off));
+        sizes.push_back(actual_size(sz));
+        total += sizes.back();
+    }
+    out_offsets[n] = total;
+    if (total > cap)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "needles need " + std::to_string(total) + " bytes, cap " +
+                                                  std::to_string(cap));
+    if (offs.empty()) return HEC_OK;
+    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
+    return read_ranges(base, sh, large, small, offs.data(), sizes.data(), offs.size(), out);
+}
+
+// maybe_load_volume_info (helyim-ec/src/volume_info.rs:107-119): absent file
+// -> none; a VolumeInfo whose `files` list is empty -> none; else its version.
+// The JSON is the serde form hec_save_volume_info writes; only the two fields
+// the decision needs are read.
+int maybe_load_version(const std::string& filename, bool* found, uint32_t* version) {
+    *found = false;
+    const int fd = ::open(filename.c_str(), O_RDONLY);
+    if (fd < 0) {
+        if (errno == ENOENT) return HEC_OK;
+        return io("open " + filename);
+    }
+    std::string text;
+    char buf[4096];
+    for (;;) {
+        const ssize_t r = ::read(fd, buf, sizeof buf);
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0) {
+            ::close(fd);
+            return io("read " + filename);
+        }
+        if (r == 0) break;
+        text.append(buf, size_t(r));
+    }
+    ::close(fd);
+    auto skip_ws = [&](size_t i) {
+        while (i < text.size() && (text[i] == ' ' || text[i] == '\n' || text[i] == '\t' || text[i] == '\r')) ++i;
+        return i;
+    };
+    auto value_at = [&](const char* key) -> size_t {  // index of the value of "key", or npos
+        const size_t k = text.find(std::string("\"") + key + "\"");
+        if (k == std::string::npos) return k;
+        size_t i = skip_ws(k + std::strlen(key) + 2);
+        if (i >= text.size() || text[i] != ':') return std::string::npos;
+        return skip_ws(i + 1);
+    };
+    const size_t fi = skip_ws(0);
+    if (fi >= text.size() || text[fi] != '{') return fail(HEC_ERR_IO, filename + ": not a JSON object");
+    const size_t files = value_at("files");
+    if (files == std::string::npos || text.compare(files, 1, "[") != 0 ||
+        (skip_ws(files + 1) < text.size() && text[skip_ws(files + 1)] == ']'))
+        return HEC_OK;  // files empty (or defaulted): none
+    const size_t v = value_at("version");
+    uint32_t ver = 0;
+    for (size_t i = v; v != std::string::npos && i < text.size() && text[i] >= '0' && text[i] <= '9'; ++i)
+        ver = ver * 10 + uint32_t(text[i] - '0');
+    *found = true;
+    *version = ver;
+    return HEC_OK;
+}
+
 }  // namespace
 }  // namespace hec
 
 using namespace hec;
+
+// A mounted EC volume (EcVolume, helyim-ec/src/volume/mod.rs:30-171): .ecx
+// and .ecj held open, every local base.ecNN mounted, block geometry fixed.
+struct hec_ec_volume {
+    std::string base;
+    uint64_t large = 0, small = 0;
+    Shards shards;
+    Ecx ecx;
+    int ecj_fd = -1;
+    uint32_t version = 2;
+    std::mutex mu;  // serialises deletes (.ecx tombstone + .ecj append)
+    ~hec_ec_volume() {
+        if (ecj_fd >= 0) ::close(ecj_fd);
+    }
+};
 
 extern "C" {
 
@@ -322,19 +451,12 @@ int hec_read_ec_needle_ex(const char* base_filename, uint64_t large_block_size, 
                           uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out) {
     if (!base_filename || !n_out) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
     *n_out = 0;
-    uint32_t off;
-    int32_t sz;
-    int rc = hec_find_needle_from_ecx(base_filename, needle_id, &off, &sz);
+    Ecx ecx;
+    int rc = ecx.open(base_filename);
     if (rc) return rc;
-    if (sz < 0)  // Size::is_deleted
-        return fail(HEC_ERR_NEEDLE_NOT_FOUND, "Needle " + std::to_string(needle_id) + " not found");
-    const uint64_t a_off = actual_offset(off), a_size = actual_size(sz);
-    *n_out = size_t(a_size);
-    if (a_size > cap)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "needle needs " + std::to_string(a_size) + " bytes, cap " +
-                                                  std::to_string(cap));
-    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
-    return read_ranges(base_filename, large_block_size, small_block_size, &a_off, &a_size, 1, out);
+    Shards sh;
+    if ((rc = sh.open(base_filename))) return rc;
+    return read_needle(base_filename, ecx, sh, large_block_size, small_block_size, needle_id, out, cap, n_out);
 }
 
 int hec_read_ec_needles(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
@@ -345,35 +467,100 @@ int hec_read_ec_needles(const char* base_filename, uint64_t large_block_size, ui
     Ecx ecx;
     int rc = ecx.open(base_filename);
     if (rc) return rc;
-    std::vector<uint64_t> offs, sizes;
-    uint64_t total = 0;
-    for (size_t i = 0; i < n; ++i) {
-        uint32_t off;
-        int32_t sz;
-        out_offsets[i] = total;
-        rc = ecx.find(needle_ids[i], &off, &sz);
-        if (rc > 0) return rc;  // I/O error on .ecx
-        if (rc < 0) {
-            statuses[i] = HEC_ERR_IO;  // not in .ecx (io::ErrorKind::NotFound)
-            continue;
-        }
-        if (sz < 0) {
-            statuses[i] = HEC_ERR_NEEDLE_NOT_FOUND;
-            continue;
-        }
-        statuses[i] = HEC_OK;
-        offs.push_back(actual_offset(off));
-        sizes.push_back(actual_size(sz));
-        total += sizes.back();
+    Shards sh;
+    if ((rc = sh.open(base_filename))) return rc;
+    return read_needles(base_filename, ecx, sh, large_block_size, small_block_size, needle_ids, n, out, cap,
+                        out_offsets, statuses);
+}
+
+int hec_ec_volume_open_ex(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                          hec_ec_volume_t** out) {
+    if (!base_filename || !out) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    if (large_block_size == 0 || small_block_size == 0)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "block sizes must be > 0");
+    std::unique_ptr<hec_ec_volume> v(new hec_ec_volume());
+    v->base = base_filename;
+    v->large = large_block_size;
+    v->small = small_block_size;
+    // EcVolume::new (volume/mod.rs:45-92): .ecx read-write, .ecj read-write + create
+    int rc = v->ecx.open(v->base, true);
+    if (rc) return rc;
+    v->ecj_fd = ::open((v->base + ".ecj").c_str(), O_RDWR | O_CREAT, 0644);
+    if (v->ecj_fd < 0) return fail(HEC_ERR_IO, "open " + v->base + ".ecj: " + std::strerror(errno));
+    // .vif: load the version, or write the default VolumeInfo (version 2)
+    bool found = false;
+    uint32_t ver = 0;
+    if ((rc = maybe_load_version(v->base + ".vif", &found, &ver))) return rc;
+    if (found) {
+        v->version = ver;
+    } else {
+        struct stat st;
+        if (::stat((v->base + ".vif").c_str(), &st) == 0 && !(st.st_mode & 0200))  // check_file: not writable
+            return fail(HEC_ERR_IO, v->base + ".vif not writable.");
+        if ((rc = hec_save_volume_info((v->base + ".vif").c_str(), 2))) return rc;
+        v->version = 2;
     }
-    out_offsets[n] = total;
-    if (total > cap)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "needles need " + std::to_string(total) + " bytes, cap " +
-                                                  std::to_string(cap));
-    if (offs.empty()) return HEC_OK;
-    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
-    return read_ranges(base_filename, large_block_size, small_block_size, offs.data(), sizes.data(), offs.size(),
-                       out);
+    // add_ec_shard for every local shard file (mounted by the store)
+    if ((rc = v->shards.open(v->base))) return rc;
+    *out = v.release();
+    return HEC_OK;
+}
+
+int hec_ec_volume_open(const char* base_filename, hec_ec_volume_t** out) {
+    return hec_ec_volume_open_ex(base_filename, uint64_t(1) << 30, uint64_t(1) << 20, out);
+}
+
+void hec_ec_volume_close(hec_ec_volume_t* vol) { delete vol; }
+
+uint32_t hec_ec_volume_version(const hec_ec_volume_t* vol) { return vol ? vol->version : 0; }
+
+uint32_t hec_ec_volume_shard_bits(const hec_ec_volume_t* vol) {
+    uint32_t bits = 0;
+    for (int i = 0; vol && i < kTotalShards; ++i)
+        if (vol->shards.fd[i] >= 0) bits |= 1u << i;
+    return bits;
+}
+
+int hec_ec_volume_find_needle(const hec_ec_volume_t* vol, uint64_t needle_id, uint32_t* offset, int32_t* size) {
+    if (!vol || !offset || !size) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    const int rc = vol->ecx.find(needle_id, offset, size);
+    if (rc < 0) return fail(HEC_ERR_IO, "Needle " + std::to_string(needle_id) + " is not found");
+    return rc;
+}
+
+int hec_ec_volume_delete_needle(hec_ec_volume_t* vol, uint64_t needle_id) {
+    if (!vol) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    std::lock_guard<std::mutex> lk(vol->mu);
+    // delete_needle_from_ecx (volume/mod.rs:157-171): tombstone the size in .ecx
+    // (mark_needle_deleted, lib.rs:88-93), then append the id to .ecj
+    uint32_t off;
+    int32_t sz;
+    uint64_t entry = 0;
+    int rc = vol->ecx.find(needle_id, &off, &sz, &entry);
+    if (rc < 0) return fail(HEC_ERR_IO, "Needle " + std::to_string(needle_id) + " is not found");
+    if (rc) return rc;
+    const uint8_t tomb[4] = {0xFF, 0xFF, 0xFF, 0xFF};  // TOMBSTONE_FILE_SIZE = -1, big-endian
+    if (::pwrite(vol->ecx.fd, tomb, 4, off_t(entry * kEntry + 12)) != 4) return io("write " + vol->ecx.name);
+    struct stat st;
+    if (::fstat(vol->ecj_fd, &st) != 0) return io("stat " + vol->base + ".ecj");
+    uint8_t id[8];
+    for (int i = 0; i < 8; ++i) id[i] = uint8_t(needle_id >> (56 - 8 * i));
+    if (::pwrite(vol->ecj_fd, id, 8, st.st_size) != 8) return io("write " + vol->base + ".ecj");
+    return HEC_OK;
+}
+
+int hec_ec_volume_read_needle(hec_ec_volume_t* vol, uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out) {
+    if (!vol || !n_out) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    return read_needle(vol->base, vol->ecx, vol->shards, vol->large, vol->small, needle_id, out, cap, n_out);
+}
+
+int hec_ec_volume_read_needles(hec_ec_volume_t* vol, const uint64_t* needle_ids, size_t n, uint8_t* out, size_t cap,
+                               uint64_t* out_offsets, int* statuses) {
+    if (!vol || !out_offsets || !statuses || (n && !needle_ids))
+        return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    return read_needles(vol->base, vol->ecx, vol->shards, vol->large, vol->small, needle_ids, n, out, cap,
+                        out_offsets, statuses);
 }
 
 int hec_read_ec_needle(const char* base_filename, uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out) {

@@ -283,6 +283,38 @@ int hec_read_ec_needles(const char* base_filename, uint64_t large_block_size, ui
                         const uint64_t* needle_ids, size_t n, uint8_t* out, size_t cap, uint64_t* out_offsets,
                         int* statuses);
 
+/* ---- mounted EC volume (EcVolume, helyim-ec/src/volume/mod.rs:30-171) -------
+ * A handle that keeps the volume's files open for a stream of reads, so a
+ * needle read costs the lookup and the preads only. */
+typedef struct hec_ec_volume hec_ec_volume_t;
+/* EcVolume::new (mod.rs:45-92) + add_ec_shard (mod.rs:94-108) for every local
+ * base.ecNN: opens base.ecx read-write (missing -> HEC_ERR_IO), opens or
+ * creates base.ecj, loads the version from base.vif -- a missing .vif or one
+ * whose `files` list is empty (maybe_load_volume_info, volume_info.rs:107-119)
+ * is (re)written as the default VolumeInfo with version 2 -- and mounts every
+ * shard file present. 1 GiB / 1 MiB blocks (ERASURE_CODING_*_BLOCK_SIZE). */
+int hec_ec_volume_open(const char* base_filename, hec_ec_volume_t** out);
+/* hec_ec_volume_open with explicit block sizes (tests exercise large rows). */
+int hec_ec_volume_open_ex(const char* base_filename, uint64_t large_block_size, uint64_t small_block_size,
+                          hec_ec_volume_t** out);
+void hec_ec_volume_close(hec_ec_volume_t* vol);
+/* EcVolume::version; 0 for a null handle. */
+uint32_t hec_ec_volume_version(const hec_ec_volume_t* vol);
+/* Bit i set = shard i mounted. */
+uint32_t hec_ec_volume_shard_bits(const hec_ec_volume_t* vol);
+/* find_needle_from_ecx (mod.rs:153-155), as hec_find_needle_from_ecx. */
+int hec_ec_volume_find_needle(const hec_ec_volume_t* vol, uint64_t needle_id, uint32_t* offset, int32_t* size);
+/* delete_needle_from_ecx (mod.rs:157-171): the entry's size becomes the
+ * tombstone (-1) in .ecx (mark_needle_deleted, lib.rs:88-93) and the id is
+ * appended to .ecj (8 bytes, big-endian). Absent id -> HEC_ERR_IO ("Needle {id}
+ * is not found"), nothing written. Deletes are serialised per handle. */
+int hec_ec_volume_delete_needle(hec_ec_volume_t* vol, uint64_t needle_id);
+/* hec_read_ec_needle / hec_read_ec_needles against the mounted files (same
+ * arguments, statuses and errors). Reads may run concurrently on one handle. */
+int hec_ec_volume_read_needle(hec_ec_volume_t* vol, uint64_t needle_id, uint8_t* out, size_t cap, size_t* n_out);
+int hec_ec_volume_read_needles(hec_ec_volume_t* vol, const uint64_t* needle_ids, size_t n, uint8_t* out, size_t cap,
+                               uint64_t* out_offsets, int* statuses);
+
 /* ---- tuning / introspection ----------------------------------------------- */
 /* Kernel launch configuration (process-wide; speed only, results identical):
  * vec_per_thread 16-byte vectors per lane per chunk (1, 2, 4); max_blocks

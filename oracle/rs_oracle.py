@@ -675,3 +675,45 @@ def read_ec_needle(base: str, needle_id: int, large=ERASURE_CODING_LARGE_BLOCK_S
     body = 16 + (size & 0xFFFFFFFF) + 4                 # Size::actual_size
     actual_size = (body + (8 - body % 8)) & 0xFFFFFFFF
     return read_ec_data(base, [(actual_offset, actual_size)], large, small)
+
+
+# ---- EcVolume (helyim-ec/src/volume/mod.rs:30-171) ---------------------------
+
+def ec_volume_open_version(base: str) -> int:
+    """EcVolume::new's .vif step (mod.rs:66-77) with maybe_load_volume_info
+    (volume_info.rs:107-119): a missing .vif, or one whose `files` list is
+    empty, is (re)written as VolumeInfo{version: 2}; else its version. Also
+    creates .ecj (OpenOptions::create, mod.rs:59-64)."""
+    import json
+    open(base + ".ecj", "ab").close()
+    vif = base + ".vif"
+    if os.path.exists(vif):
+        info = json.loads(open(vif, "rb").read())
+        if info.get("files"):
+            return int(info.get("version", 0))
+    with open(vif, "wb") as f:
+        f.write(volume_info_json(2))
+    return 2
+
+
+def ec_volume_delete_needle(base: str, needle_id: int) -> None:
+    """delete_needle_from_ecx (mod.rs:157-171): tombstone the entry's size in
+    .ecx (mark_needle_deleted, lib.rs:88-93), append the id to .ecj."""
+    with open(base + ".ecx", "r+b") as ecx:
+        raw = ecx.read()
+        lo, hi = 0, len(raw) // 16
+        while lo < hi:
+            mid = (lo + hi) // 2
+            key = _struct.unpack(">Q", raw[mid * 16:mid * 16 + 8])[0]
+            if key == needle_id:
+                ecx.seek(mid * 16 + 12)
+                ecx.write(_struct.pack(">i", -1))
+                break
+            if key < needle_id:
+                lo = mid + 1
+            else:
+                hi = mid
+        else:
+            raise IoError("Needle %d is not found" % needle_id)
+    with open(base + ".ecj", "ab") as f:
+        f.write(_struct.pack(">Q", needle_id))

@@ -284,3 +284,120 @@ def test_degraded_read_too_many_lost(gpu, tmp_path):
     assert isinstance(ei.value.inner, H.TooFewShardsPresent)
     with pytest.raises(O.RSError):
         O.read_ec_data(base, [(100, 10)], LARGE, SMALL)
+
+
+# ---- mounted volume handle (EcVolume, helyim-ec/src/volume/mod.rs) ------------
+
+def test_ec_volume_mount_vif_and_ecj(tmp_path):
+    """EcVolume::new: .ecj created, .vif written with version 2 when missing or
+    when its `files` list is empty (maybe_load_volume_info), kept otherwise."""
+    import json
+    import os
+    import helyim_amd as H
+    base, _, _ = _needle_volume(tmp_path)
+    twin = str(tmp_path / "twin")
+    import shutil
+    for ext in (".ecx",):
+        shutil.copyfile(base + ext, twin + ext)
+    for b in (base, twin):
+        for ext in (".ecj", ".vif"):
+            if os.path.exists(b + ext):
+                os.remove(b + ext)
+    with H.EcVolume(base, LARGE, SMALL) as v:
+        assert v.version == O.ec_volume_open_version(twin) == 2
+        assert v.shard_ids() == list(range(14))
+    for ext in (".ecj", ".vif"):
+        assert open(base + ext, "rb").read() == open(twin + ext, "rb").read()
+    H.save_volume_info(base + ".vif", 3)  # files empty -> rewritten as version 2
+    with H.EcVolume(base, LARGE, SMALL) as v:
+        assert v.version == 2
+    assert open(base + ".vif", "rb").read() == O.volume_info_json(2)
+    info = {"files": [{"backend_type": "s3", "key": "k"}], "version": 3, "replication": ""}
+    open(base + ".vif", "w").write(json.dumps(info))
+    with H.EcVolume(base, LARGE, SMALL) as v:
+        assert v.version == 3
+    assert json.loads(open(base + ".vif").read()) == info
+    _drop(base, [2, 11])
+    with H.EcVolume(base, LARGE, SMALL) as v:
+        assert v.shard_ids() == [i for i in range(14) if i not in (2, 11)]
+    os.remove(base + ".ecx")
+    with pytest.raises(H.Io):
+        H.EcVolume(base, LARGE, SMALL)
+
+
+def test_ec_volume_reads_host_only(tmp_path):
+    import helyim_amd as H
+    base, dat, entries = _needle_volume(tmp_path)
+    with H.EcVolume(base, LARGE, SMALL) as v:
+        for i, (k, off, size) in enumerate(entries):
+            assert v.find_needle_from_ecx(k) == H.find_needle_from_ecx(base, k)
+            if i == 5:
+                with pytest.raises(H.NeedleNotFound):
+                    v.read_needle(k)
+                continue
+            assert v.read_needle(k) == _needle_bytes(dat, off, size)
+        got = v.read_needles([k for k, _, _ in entries] + [999999])
+        assert got[:5] + got[6:-1] == [_needle_bytes(dat, o, s) for i, (_, o, s) in enumerate(entries) if i != 5]
+        assert isinstance(got[5], H.NeedleNotFound) and isinstance(got[-1], H.Io)
+        with pytest.raises(H.Io, match="is not found"):
+            v.read_needle(123456789)
+
+
+def test_ec_volume_delete_needle(tmp_path):
+    """delete_needle_from_ecx: .ecx tombstone + .ecj append, byte-identical to
+    the oracle; the needle then reads as deleted; an absent id writes nothing."""
+    import shutil
+    import helyim_amd as H
+    base, dat, entries = _needle_volume(tmp_path)
+    twin = str(tmp_path / "twin")
+    shutil.copyfile(base + ".ecx", twin + ".ecx")
+    with H.EcVolume(base, LARGE, SMALL) as v:
+        O.ec_volume_open_version(twin)
+        for i in (0, 17, 39):
+            k = entries[i][0]
+            v.delete_needle_from_ecx(k)
+            O.ec_volume_delete_needle(twin, k)
+            with pytest.raises(H.NeedleNotFound):
+                v.read_needle(k)
+            assert v.find_needle_from_ecx(k) == (entries[i][1], -1)
+        before = (open(base + ".ecx", "rb").read(), open(base + ".ecj", "rb").read())
+        with pytest.raises(H.Io, match="is not found"):
+            v.delete_needle_from_ecx(424242)
+        assert (open(base + ".ecx", "rb").read(), open(base + ".ecj", "rb").read()) == before
+        assert v.read_needle(entries[1][0]) == _needle_bytes(dat, entries[1][1], entries[1][2])
+    for ext in (".ecx", ".ecj"):
+        assert open(base + ext, "rb").read() == open(twin + ext, "rb").read()
+    H.rebuild_ecx_file(base)  # replaying the .ecj is idempotent on the tombstones
+    O.rebuild_ecx_file(twin)
+    assert open(base + ".ecx", "rb").read() == open(twin + ".ecx", "rb").read()
+
+
+@pytest.mark.gpu
+def test_ec_volume_degraded_reads_concurrent(gpu, tmp_path):
+    """Degraded reads through one mounted handle from 8 threads at once."""
+    import threading
+    import helyim_amd as H
+    base, dat, entries = _needle_volume(tmp_path, n_needles=200, seed=7)
+    _drop(base, [1, 4, 8, 13])
+    errors = []
+    with H.EcVolume(base, LARGE, SMALL) as v:
+        def worker(t):
+            try:
+                for i in range(t, len(entries), 8):
+                    k, off, size = entries[i]
+                    if i == 5:
+                        continue
+                    if v.read_needle(k) != _needle_bytes(dat, off, size):
+                        errors.append(k)
+                got = v.read_needles([k for k, _, _ in entries[t::8]])
+                for (k, off, size), g in zip(entries[t::8], got):
+                    if not isinstance(g, Exception) and g != _needle_bytes(dat, off, size):
+                        errors.append(k)
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    assert not errors

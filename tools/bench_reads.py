@@ -8,6 +8,8 @@ removed, and --n random needles are read three ways, outputs compared:
                 reconstruct on one CPU thread (erasure_coding/mod.rs:303-491)
   gpu_single -- hec_read_ec_needle, one call per needle
   gpu_batch  -- hec_read_ec_needles, all needles in one call (one GPU batch)
+  vol_single -- hec_ec_volume_read_needle on a mounted EcVolume handle
+  vol_batch  -- hec_ec_volume_read_needles on the handle
 python tools/bench_reads.py [--gib 2] [--n 4000]
 """
 import argparse
@@ -95,16 +97,35 @@ def main():
     offs = (ctypes.c_uint64 * (n + 1))()
     st = (ctypes.c_int * n)()
     big = ctypes.create_string_buffer(payload)
-    H.lib.hec_read_ec_needles(name, 1 << 30, 1 << 20, ids, min(n, 8), big, payload, offs, st)  # warm-up
+    H.lib.hec_read_ec_needles(name, 1 << 30, 1 << 20, ids, n, big, payload, offs, st)  # warm-up: staging sized
     t0 = time.perf_counter()
     rc = H.lib.hec_read_ec_needles(name, 1 << 30, 1 << 20, ids, n, big, payload, offs, st)
     t_batch = time.perf_counter() - t0
     raw = big.raw
     ok_batch = rc == 0 and all(st[i] == 0 and raw[offs[i]:offs[i + 1]] == want[i] for i in range(n))
 
-    for key, t in (("cpu_c_1thread", t_cpu), ("gpu_single", t_single), ("gpu_batch", t_batch)):
+    # mounted volume: files opened once
+    vol = ctypes.c_void_p()
+    assert H.lib.hec_ec_volume_open(name, ctypes.byref(vol)) == 0
+    H.lib.hec_ec_volume_read_needle(vol, sel[0][0], buf, cap, ctypes.byref(nout))  # warm-up
+    vsingle = []
+    t0 = time.perf_counter()
+    for nid, _, _ in sel:
+        rc = H.lib.hec_ec_volume_read_needle(vol, nid, buf, cap, ctypes.byref(nout))
+        vsingle.append(rc == 0 and buf.raw[:nout.value])
+    t_vsingle = time.perf_counter() - t0
+    ok_vsingle = all(b == w for b, w in zip(vsingle, want))
+    t0 = time.perf_counter()
+    rc = H.lib.hec_ec_volume_read_needles(vol, ids, n, big, payload, offs, st)
+    t_vbatch = time.perf_counter() - t0
+    raw = big.raw
+    ok_vbatch = rc == 0 and all(st[i] == 0 and raw[offs[i]:offs[i + 1]] == want[i] for i in range(n))
+    H.lib.hec_ec_volume_close(vol)
+
+    for key, t in (("cpu_c_1thread", t_cpu), ("gpu_single", t_single), ("gpu_batch", t_batch),
+                   ("vol_single", t_vsingle), ("vol_batch", t_vbatch)):
         out[key] = {"s": round(t, 4), "needles_per_s": round(n / t, 1), "GiB_s": round(payload / t / 2**30, 3)}
-    out["identical_outputs"] = bool(ok_cpu and ok_single and ok_batch)
+    out["identical_outputs"] = bool(ok_cpu and ok_single and ok_batch and ok_vsingle and ok_vbatch)
     print(json.dumps(out), flush=True)
     for f in os.listdir(tmp):
         os.remove(os.path.join(tmp, f))

@@ -111,21 +111,22 @@ using CompactTake = std::function<void(size_t job, int shard, const uint8_t* src
 int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& jobs, const CompactFill& fill,
                             const CompactTake& take);
 
-// Run fn(i) for i in [0, n) on up to 16 threads (host memcpy of staging).
+// Run fn(i) for i in [0, n) on the library's persistent host worker pool
+// (host memcpy of staging): up to 16 threads, at least 1 MiB of `bytes` per
+// thread and 4 MiB in all (below that, waking workers costs more than the
+// copy saves: measured at 256 KiB shards, tools/bench_latency.py).
+// Concurrent callers do not wait for each other: a call that finds the pool
+// busy runs serially on its own thread.
+void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>& fn);
+
 template <typename F>
 void parallel_for(size_t n, uint64_t bytes, F fn) {
-    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const unsigned nt = unsigned(std::min<uint64_t>(hw, std::max<uint64_t>(1, bytes >> 22)));  // >= 4 MiB/thread
-    if (nt <= 1 || n < 2) {
+    const unsigned nt = unsigned(std::min<uint64_t>(16, std::max<uint64_t>(1, bytes >> 20)));  // >= 1 MiB/thread
+    if (nt <= 1 || n < 2 || bytes < (uint64_t(4) << 20)) {
         for (size_t i = 0; i < n; ++i) fn(i);
         return;
     }
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t)
-        th.emplace_back([&, t] {
-            for (size_t i = t; i < n; i += nt) fn(i);
-        });
-    for (auto& x : th) x.join();
+    pool_run(n, nt, std::function<void(size_t)>(fn));
 }
 
 // Run one plan set over a strided batch (plan 0 for every stripe unless masks).

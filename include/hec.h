@@ -349,7 +349,7 @@ int hec_set_encode_kernel(int kind);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables
- * staging. Default 4 MiB (the measured crossover). Speed only. Returns HEC_OK. */
+ * staging. Default 16 MiB (the measured crossover). Speed only. Returns HEC_OK. */
 int hec_set_host_staging(uint64_t max_bytes);
 /* Version string of the library build. */
 const char* hec_version(void);

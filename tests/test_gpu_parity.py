@@ -95,7 +95,7 @@ def test_host_calls_staged_and_direct(gpu, staging, k, m):
     rng = np.random.default_rng(11 * k + m)
     rs, ors = H.ReedSolomon(k, m), O.ReedSolomon(k, m)
     try:
-        for L in (1, 17, 4096 + 3, 65536 + 7, (1 << 20) + 5):
+        for L in (1, 17, 4096 + 3, 65536 + 7, (128 << 10) + 1, 256 << 10, (1 << 20) + 5):
             lim = {"off": 0, "on": 1 << 40, "edge": k * L}[staging]
             H.lib.hec_set_host_staging(lim)
             data = [_rand(rng, L) for _ in range(k)]
@@ -126,7 +126,7 @@ def test_host_calls_staged_and_direct(gpu, staging, k, m):
             with pytest.raises(H.IncorrectShardSize):
                 rs.reconstruct([None, np.zeros(L + 1, np.uint8)] + ref[2:])
     finally:
-        H.lib.hec_set_host_staging(4 << 20)
+        H.lib.hec_set_host_staging(16 << 20)
 
 
 def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):

@@ -374,6 +374,20 @@ int Scratch::reserve_host(size_t bytes) {
     return HEC_OK;
 }
 
+bool& zero_copy_enabled() {
+    static bool on = true;
+    return on;
+}
+
+uint8_t* pinned_device_ptr(void* host) {
+    void* d = nullptr;
+    if (!host || hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t*>(d);
+}
+
 uint64_t& host_staging_max() {
     static uint64_t v = uint64_t(16) << 20;  // measured crossover
     return v;
@@ -427,12 +441,19 @@ static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* co
         if ((rc = sc->reserve_host(size_t(Lp) * rs->n))) return rc;
         parallel_for(size_t(rs->k), uint64_t(rs->k) * L,
                      [&](size_t i) { std::memcpy(sc->hbuf + i * Lp, data[i], L); });
-        HEC_HIP(hipMemcpyAsync(sc->dbuf, sc->hbuf, size_t(rs->k) * Lp, hipMemcpyHostToDevice, sc->stream));
-        if ((rc = run_apply(gd->encode, uint32_t(rs->k), sc->dbuf, 0, Lp, par, 0, Lp, round_up(L, 16), 1,
-                            nullptr, nullptr, sc->stream)))
-            return rc;
         uint8_t* hpar = sc->hbuf + size_t(rs->k) * Lp;
-        HEC_HIP(hipMemcpyAsync(hpar, par, size_t(rs->m - 1) * Lp + L, hipMemcpyDeviceToHost, sc->stream));
+        uint8_t* zh = zero_copy_enabled() ? pinned_device_ptr(sc->hbuf) : nullptr;
+        if (zh) {  // the kernel reads the packed shards and writes parity over PCIe
+            if ((rc = run_apply(gd->encode, uint32_t(rs->k), zh, 0, Lp, zh + size_t(rs->k) * Lp, 0, Lp,
+                                round_up(L, 16), 1, nullptr, nullptr, sc->stream)))
+                return rc;
+        } else {
+            HEC_HIP(hipMemcpyAsync(sc->dbuf, sc->hbuf, size_t(rs->k) * Lp, hipMemcpyHostToDevice, sc->stream));
+            if ((rc = run_apply(gd->encode, uint32_t(rs->k), sc->dbuf, 0, Lp, par, 0, Lp, round_up(L, 16), 1,
+                                nullptr, nullptr, sc->stream)))
+                return rc;
+            HEC_HIP(hipMemcpyAsync(hpar, par, size_t(rs->m - 1) * Lp + L, hipMemcpyDeviceToHost, sc->stream));
+        }
         HEC_HIP(hipStreamSynchronize(sc->stream));
         parallel_for(size_t(rs->m), uint64_t(rs->m) * L,
                      [&](size_t j) { std::memcpy(dst_of(int(j)), hpar + j * Lp, L); });

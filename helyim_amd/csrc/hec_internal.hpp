@@ -92,6 +92,12 @@ struct Scratch {
 };
 int device_scratch(Scratch** out);
 
+// Zero-copy switch (hec_set_host_zero_copy): pinned host memory the GPU can
+// address is coded by the kernels in place over PCIe instead of being copied.
+bool& zero_copy_enabled();
+// Device address of a hipHostMalloc'd pinned buffer (nullptr if unavailable).
+uint8_t* pinned_device_ptr(void* host);
+
 // Host calls whose k * shard_len input is at most this many bytes go through
 // pinned staging (one H2D, one D2H) instead of one pageable copy per shard.
 uint64_t& host_staging_max();

@@ -84,6 +84,39 @@ hipError_t copy2d(void* dst, uint64_t dpitch, const void* src, uint64_t spitch, 
     return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s);
 }
 
+// Zero-copy: pinned host memory that the GPU can address directly
+// (hipHostMalloc / torch pin_memory) is handed to the kernel as is, so the
+// kernel's loads and stores cross PCIe themselves -- no staging slots, no SDMA
+// copies, both directions at once. Measured 51 GiB/s of data encoded vs 41-44
+// for the copy pipeline (tools/zerocopy_probe.hip). The whole
+// [p, p + span) must be one registered host range; anything else (pageable
+// memory, device memory, a range running past the allocation) takes the copy
+// pipeline. hec_set_host_zero_copy(0) disables it (measurement).
+bool host_device_view(const void* p, uint64_t span, uint8_t** dev) {
+    if (!zero_copy_enabled() || span == 0) return false;
+    hipPointerAttribute_t a{}, b{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const void* last = static_cast<const uint8_t*>(p) + (span - 1);
+    if (hipPointerGetAttributes(&b, last) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (a.type != hipMemoryTypeHost || b.type != hipMemoryTypeHost || !a.devicePointer || !b.devicePointer)
+        return false;
+    if (static_cast<uint8_t*>(b.devicePointer) - static_cast<uint8_t*>(a.devicePointer) != int64_t(span - 1))
+        return false;
+    *dev = static_cast<uint8_t*>(a.devicePointer);
+    return true;
+}
+
+// bytes from the first to the last byte touched by a strided batch
+uint64_t batch_span(uint64_t stripe_stride, uint64_t shard_stride, uint32_t shards, uint64_t len, uint32_t stripes) {
+    return uint64_t(stripes - 1) * stripe_stride + uint64_t(shards - 1) * shard_stride + len;
+}
+
 uint32_t chunk_stripes(uint64_t shard_len, int n, uint32_t n_stripes) {
     uint64_t c = std::max<uint64_t>(1, kChunkBytes / (uint64_t(n) * shard_len));
     return uint32_t(std::min<uint64_t>(c, n_stripes));
@@ -109,6 +142,18 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
     if ((rc = pipeline(&p))) return rc;
     std::lock_guard<std::mutex> lk(p->mu);
     const int k = rs->k, m = rs->m;
+    uint8_t *zd, *zp;
+    if (host_device_view(h_data, batch_span(data_stripe_stride, data_shard_stride, k, shard_len, n_stripes), &zd) &&
+        host_device_view(h_parity, batch_span(parity_stripe_stride, parity_shard_stride, m, shard_len, n_stripes),
+                         &zp)) {
+        if ((rc = p->reserve(0, 1))) return rc;
+        if ((rc = run_apply(gd->encode, uint32_t(k), zd, data_stripe_stride, data_shard_stride, zp,
+                            parity_stripe_stride, parity_shard_stride, shard_len, n_stripes, nullptr, nullptr,
+                            p->streams[0])))
+            return rc;
+        HEC_HIP(hipStreamSynchronize(p->streams[0]));
+        return HEC_OK;
+    }
     const uint64_t Lp = (shard_len + 255) / 256 * 256;  // device shard pitch
     const uint32_t C = chunk_stripes(Lp, rs->n, n_stripes);
     if ((rc = p->reserve(size_t(C) * rs->n * Lp, 1))) return rc;
@@ -147,12 +192,33 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
     if ((rc = pipeline(&p))) return rc;
     std::lock_guard<std::mutex> lk(p->mu);
     const int k = rs->k, n = rs->n;
+    const uint32_t full = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
+    uint8_t* zs;
+    if (host_device_view(h_shards, batch_span(stripe_stride, shard_stride, n, shard_len, n_stripes), &zs)) {
+        // masks to the device (the caller's array may be pageable), then one
+        // decode over the pinned host shards in place
+        if ((rc = p->reserve(0, n_stripes))) return rc;
+        if ((rc = ensure_dense_decode(rs, gd, p->streams[0]))) return rc;
+        uint32_t bad = 0;
+        for (uint32_t s = 0; s < n_stripes; ++s) {
+            const uint32_t mask = h_present_masks[s] & full;
+            p->mask_host[0][s] = mask;
+            bad += __builtin_popcount(mask) < k ? 1u : 0u;
+        }
+        HEC_HIP(hipMemcpyAsync(p->mask_dev[0], p->mask_host[0], size_t(n_stripes) * 4, hipMemcpyHostToDevice,
+                               p->streams[0]));
+        if ((rc = run_apply(gd->decode_dense, uint32_t(k), zs, stripe_stride, shard_stride, zs, stripe_stride,
+                            shard_stride, shard_len, n_stripes, p->mask_dev[0], nullptr, p->streams[0])))
+            return rc;
+        HEC_HIP(hipStreamSynchronize(p->streams[0]));
+        if (n_bad_stripes) *n_bad_stripes = bad;
+        return HEC_OK;
+    }
     const uint64_t Lp = (shard_len + 255) / 256 * 256;
     const uint32_t C = chunk_stripes(Lp, n, n_stripes);
     if ((rc = p->reserve(size_t(C) * n * Lp, C))) return rc;
     if ((rc = ensure_dense_decode(rs, gd, p->streams[0]))) return rc;
     const uint64_t dstripe = uint64_t(n) * Lp;
-    const uint32_t full = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
     uint32_t bad = 0;
     for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
         const uint32_t c = std::min(C, n_stripes - s0);
@@ -210,6 +276,11 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
     }
     for (int q = 0; q < kDepth; ++q) HEC_HIP(hipStreamSynchronize(p->streams[q]));
     if (n_bad_stripes) *n_bad_stripes = bad;
+    return HEC_OK;
+}
+
+int hec_set_host_zero_copy(int on) {
+    zero_copy_enabled() = on != 0;
     return HEC_OK;
 }
 

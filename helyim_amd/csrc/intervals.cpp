@@ -126,9 +126,12 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     const size_t map_off = (items_bytes + 255) / 256 * 256;
     std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
     HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, sc->stream));
-    HEC_HIP(hipMemcpyAsync(sc->dev, sc->host, in_total, hipMemcpyHostToDevice, sc->stream));
+    // zero-copy: the kernel reads the packed survivors and writes the rebuilt
+    // shards in the pinned staging itself (no H2D / D2H of the payload)
+    uint8_t* zh = zero_copy_enabled() ? pinned_device_ptr(sc->host) : nullptr;
+    if (!zh) HEC_HIP(hipMemcpyAsync(sc->dev, sc->host, in_total, hipMemcpyHostToDevice, sc->stream));
     RaggedArgs ra{};
-    ra.base = sc->dev;
+    ra.base = zh ? zh : sc->dev;
     ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
     ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
     ra.n_blocks = uint32_t(block_item.size());
@@ -136,8 +139,9 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     ra.lut = gd->decode_dense.lut;
     ra.compact = 1;
     HEC_HIP(launch_rs104_ragged(ra, true, sc->stream));
-    HEC_HIP(hipMemcpyAsync(sc->host + in_total, sc->dev + in_total, total - in_total, hipMemcpyDeviceToHost,
-                           sc->stream));
+    if (!zh)
+        HEC_HIP(hipMemcpyAsync(sc->host + in_total, sc->dev + in_total, total - in_total, hipMemcpyDeviceToHost,
+                               sc->stream));
     HEC_HIP(hipStreamSynchronize(sc->stream));
     // hand back the erased shards
     parallel_for(jobs.size(), total - in_total, [&](size_t j) {

@@ -152,10 +152,11 @@ int hec_gpu_reconstruct_batch(const hec_rs_t* rs, uint8_t* d_shards, uint64_t st
 
 /* ---- host-memory batches (the path helyim runs: bytes start and end in host
  * memory, encoder.rs:169-195 / 263-304) -------------------------------------
- * Same strided layout as above but on HOST pointers. Chunks of stripes are
- * pipelined H2D -> kernel -> D2H over 3 HIP streams so copies overlap the
- * kernels; synchronous on return. Pin the host buffers (hipHostMalloc,
- * torch pin_memory) for full PCIe rate; pageable memory works, slower. */
+ * Same strided layout as above but on HOST pointers; synchronous on return.
+ * Pinned buffers the GPU can address (hipHostMalloc, torch pin_memory) are
+ * coded zero-copy: the kernel reads and writes them over PCIe directly.
+ * Other memory (pageable) is pipelined H2D -> kernel -> D2H over 3 HIP
+ * streams so the copies overlap the kernels. */
 int hec_host_encode_batch(const hec_rs_t* rs,
                           const uint8_t* h_data, uint64_t data_stripe_stride, uint64_t data_shard_stride,
                           uint8_t* h_parity, uint64_t parity_stripe_stride, uint64_t parity_shard_stride,
@@ -351,6 +352,9 @@ int hec_set_encode_kernel(int kind);
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables
  * staging. Default 16 MiB (the measured crossover). Speed only. Returns HEC_OK. */
 int hec_set_host_staging(uint64_t max_bytes);
+/* Host batches on pinned memory: 1 = zero-copy kernels (default), 0 = the
+ * copy pipeline. Speed only; identical results. Returns HEC_OK. */
+int hec_set_host_zero_copy(int on);
 /* Version string of the library build. */
 const char* hec_version(void);
 /* Name of the kernel a 16-byte-aligned RS(10,4) device batch encode of this

@@ -1,4 +1,5 @@
-"""Host-memory batches (pinned H2D -> kernel -> D2H pipeline) vs the oracle."""
+"""Host-memory batches (zero-copy kernels on pinned memory, or the pinned
+H2D -> kernel -> D2H pipeline) vs the oracle."""
 import itertools
 
 import numpy as np
@@ -8,6 +9,17 @@ from oracle import corc
 from oracle import rs_oracle as O
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["zero_copy", "copy_pipeline"])
+def host_path(request, gpu):
+    """Every host-batch test runs on both paths: pinned buffers coded in place
+    by the kernel over PCIe (default), and the H2D -> kernel -> D2H pipeline.
+    Pageable buffers take the pipeline either way."""
+    import helyim_amd as H
+    assert H.lib.hec_set_host_zero_copy(1 if request.param == "zero_copy" else 0) == 0
+    yield request.param
+    H.lib.hec_set_host_zero_copy(1)
 
 
 def _host_stripes(S, L, pin=True):

@@ -10,6 +10,16 @@ from oracle import rs_oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["zero_copy", "copies"])
+def staging_path(request, gpu):
+    """The compact staging is decoded in place by the kernel over PCIe (zero
+    copy, default) or copied H2D / D2H around the kernel."""
+    import helyim_amd as H
+    H.lib.hec_set_host_zero_copy(1 if request.param == "zero_copy" else 0)
+    yield request.param
+    H.lib.hec_set_host_zero_copy(1)
+
+
 def _stripe(rng, L):
     data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(10)]
     full = data + [np.zeros(L, np.uint8) for _ in range(4)]

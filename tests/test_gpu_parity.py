@@ -85,15 +85,18 @@ def test_reconstruct_host_api_patterns(gpu):
         rs.reconstruct([None] * 5 + full[5:])
 
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("staging", ["off", "on", "edge"])
 @pytest.mark.parametrize("k,m", [(10, 4), (3, 2)])
-def test_host_calls_staged_and_direct(gpu, staging, k, m):
-    """hec_set_host_staging picks pinned staging (one H2D + one D2H) or one
-    pageable copy per shard; both give the oracle's bytes, including the
+def test_host_calls_staged_and_direct(gpu, staging, k, m, zero_copy):
+    """hec_set_host_staging picks pinned staging (the kernel coding the staging
+    in place over PCIe, or one H2D + one D2H with zero copy off) or one
+    pageable copy per shard; all give the oracle's bytes, including the
     reconstruct_data contract."""
     import helyim_amd as H
     rng = np.random.default_rng(11 * k + m)
     rs, ors = H.ReedSolomon(k, m), O.ReedSolomon(k, m)
+    H.lib.hec_set_host_zero_copy(zero_copy)
     try:
         for L in (1, 17, 4096 + 3, 65536 + 7, (128 << 10) + 1, 256 << 10, (1 << 20) + 5):
             lim = {"off": 0, "on": 1 << 40, "edge": k * L}[staging]
@@ -127,6 +130,7 @@ def test_host_calls_staged_and_direct(gpu, staging, k, m):
                 rs.reconstruct([None, np.zeros(L + 1, np.uint8)] + ref[2:])
     finally:
         H.lib.hec_set_host_staging(16 << 20)
+        H.lib.hec_set_host_zero_copy(1)
 
 
 def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):

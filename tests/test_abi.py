@@ -121,3 +121,32 @@ def test_reconstruct_batch_validation_before_device():
     with pytest.raises(H.IncorrectShardSize) as ei:
         rs.reconstruct_batch([[None] + good[1:13] + [np.zeros(9, np.uint8)]])
     assert ei.value.stripe == 0
+
+
+def test_kernel_selection_knobs_host_only():
+    """Launch knobs validate their arguments and the encode-kernel report
+    follows the shard length (no device work)."""
+    import helyim_amd as H
+    lib = H.lib
+    try:
+        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_bs_encode_kernel")
+        assert lib.hec_encode_kernel_name(8192).decode().startswith("rs104_bs_encode_kernel")
+        assert lib.hec_encode_kernel_name(8192 + 16).decode().startswith("rs104_kernel<DEC=false>")
+        assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_kernel<DEC=false>")
+        assert lib.hec_set_encode_kernel(0) == 0
+        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_kernel<DEC=false>")
+        assert lib.hec_set_encode_kernel(3) == 0
+        assert "pipelined" in lib.hec_encode_kernel_name(1 << 20).decode()
+        assert lib.hec_set_encode_kernel(5) != 0
+        assert lib.hec_set_workgroup_size(128) == 0
+        assert lib.hec_set_encode_kernel(1) == 0
+        assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_bs_encode_kernel")  # 32 x 128 B
+        assert lib.hec_set_workgroup_size(96) != 0
+        assert lib.hec_set_kernel_mode(1) == 0
+        assert "diagnostic" in lib.hec_encode_kernel_name(1 << 20).decode()
+        assert lib.hec_set_kernel_mode(2) != 0
+        assert lib.hec_set_host_zero_copy(0) == 0 and lib.hec_set_host_zero_copy(1) == 0
+    finally:
+        lib.hec_set_kernel_mode(0)
+        lib.hec_set_workgroup_size(256)
+        lib.hec_set_encode_kernel(1)

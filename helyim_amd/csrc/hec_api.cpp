@@ -594,7 +594,7 @@ int hec_set_workgroup_size(int threads) {
 }
 
 int hec_set_encode_kernel(int kind) {
-    if (kind < 0 || kind > 4) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0..4");
+    if (kind != 0 && kind != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0 or 1");
     launch_config().bitslice = kind;
     return HEC_OK;
 }

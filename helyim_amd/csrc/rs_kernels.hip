@@ -491,8 +491,8 @@ __device__ __forceinline__ void rs104_bs_chunk(const uint8_t* in_b, uint8_t* out
     }
 }
 
-template <int TB, int MINW>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MINW))) void rs104_bs_encode_kernel(ApplyArgs a) {
+template <int TB>
+__global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
     const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
     const uint32_t stripe = item / a.chunks_per_stripe;
     const uint32_t chunk = item - stripe * a.chunks_per_stripe;
@@ -517,7 +517,7 @@ hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <int TB, int MINW>
+template <int TB>
 static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
     const uint64_t chunk = uint64_t(TB) * 2 * kVecBytes;
     a.chunks_per_stripe = uint32_t(a.len / chunk);
@@ -526,119 +526,17 @@ static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, MINW>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
-    return hipGetLastError();
-}
-
-// Bit-sliced encode, software-pipelined (persistent grid): while a workgroup
-// computes chunk c from registers, the 20 vectors per lane of its next chunk
-// stream into LDS by LDS-DMA (global_load_lds_dwordx4, no VGPRs held), so the
-// HBM reads of a wave never stop for its math. Each lane reads back only the
-// LDS slots its own DMA filled (destination = wave base + lane * 16), so no
-// barrier is needed. ORDER 0: chunk = block + it * grid (the grid sweeps the
-// batch as one narrow window); ORDER 1: each workgroup a contiguous range.
-template <int TB, int ORDER>
-__global__ __launch_bounds__(TB) void rs104_bs_pipe_kernel(ApplyArgs a) {
-    constexpr int K = 10, R = 4;
-    extern __shared__ u32x4 stage[];  // [NV][TB]
-    const uint32_t G = gridDim.x;
-    const uint32_t n = uint32_t(a.n_items);  // < 2^31 (checked by the dispatcher)
-    uint32_t it_begin, it_end, step;
-    if (ORDER == 0) {
-        it_begin = blockIdx.x;
-        it_end = n;
-        step = G;
-    } else {
-        const uint32_t per = n / G, rem = n % G;
-        it_begin = blockIdx.x * per + (blockIdx.x < rem ? blockIdx.x : rem);
-        it_end = it_begin + per + (blockIdx.x < rem ? 1 : 0);
-        step = 1;
-    }
-    if (it_begin >= it_end) return;
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 64;
-    auto issue = [&](uint32_t item) {
-        const uint32_t stripe = item / a.chunks_per_stripe;
-        const uint32_t chunk = item - stripe * a.chunks_per_stripe;
-        const uint8_t* b = a.in_base + uint64_t(stripe) * a.in_stripe + uint64_t(chunk) * (TB * 2 * kVecBytes) +
-                           threadIdx.x * kVecBytes;
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int v = 0; v < 2; ++v)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(b + uint64_t(i) * a.in_shard + v * (TB * kVecBytes)),
-                    (__attribute__((address_space(3))) void*)(stage + (2 * i + v) * TB + wbase), 16, 0, 2);
-    };
-    // The compiler does not order ds_read after an LDS-DMA to the same slots,
-    // so the waits are explicit: vmcnt(0) for the prologue DMA; at the bottom
-    // of an iteration vmcnt(8) = the next chunk's 20 DMAs have landed while
-    // this chunk's 8 stores (issued after them) may still be in flight.
-    issue(it_begin);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t item = it_begin; item < it_end; item += step) {
-        uint32_t p[K * 8];
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                const u32x4 x = stage[(2 * i + v) * TB + threadIdx.x];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) p[8 * i + 4 * v + w] = x[w];
-            }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the slots are refilled
-        const uint32_t next = item + step;
-        if (next < it_end) issue(next);
-#pragma unroll
-        for (int i = 0; i < K; ++i) transpose8(p + 8 * i);
-        uint32_t q[R * 8];
-        rs104_encode_planes(p, q);
-        const uint32_t stripe = item / a.chunks_per_stripe;
-        const uint32_t chunk = item - stripe * a.chunks_per_stripe;
-        uint8_t* ob = a.out_base + uint64_t(stripe) * a.out_stripe + uint64_t(chunk) * (TB * 2 * kVecBytes) +
-                      threadIdx.x * kVecBytes;
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            transpose8(q + 8 * j);
-            store_full(ob + uint64_t(j) * a.out_shard, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]}, true);
-            store_full(ob + uint64_t(j) * a.out_shard + TB * kVecBytes,
-                       u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]}, true);
-        }
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    }
-}
-
-template <int TB, int ORDER>
-static hipError_t launch_rs104_bs_pipe(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(TB) * 2 * kVecBytes;
-    a.chunks_per_stripe = uint32_t(a.len / chunk);
-    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
-    if (a.n_items == 0) return hipSuccess;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const size_t lds = size_t(2 * 10) * TB * kVecBytes;
-    const int per_cu = cfg.blocks_per_cu > 0 ? cfg.blocks_per_cu : int(163840 / lds);
-    uint64_t grid = uint64_t(cus) * uint64_t(per_cu);
-    if (grid > a.n_items) grid = a.n_items;
-    hipLaunchKernelGGL((rs104_bs_pipe_kernel<TB, ORDER>), dim3(uint32_t(grid)), dim3(TB), lds, stream, a);
+    hipLaunchKernelGGL((rs104_bs_encode_kernel<TB>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
     return hipGetLastError();
 }
 
 // Bit-sliced encode: shard length a multiple of 2 * TB * 16 bytes (8 KiB at
-// the default 256 threads). kind 1 = compiler's occupancy, 2 = >= 3 waves/SIMD.
+// the default 256 threads).
 static hipError_t launch_rs104_bs_cfg(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
-    if (cfg.bitslice == 3 || cfg.bitslice == 4) {  // pipelined (LDS-DMA prefetch), order 0 / 1
-        const bool o1 = cfg.bitslice == 4;
-        switch (cfg.wg_threads) {
-            case 128: return o1 ? launch_rs104_bs_pipe<128, 1>(a, cfg, stream) : launch_rs104_bs_pipe<128, 0>(a, cfg, stream);
-            default: return o1 ? launch_rs104_bs_pipe<256, 1>(a, cfg, stream) : launch_rs104_bs_pipe<256, 0>(a, cfg, stream);
-        }
-    }
-    const bool w3 = cfg.bitslice == 2;
     switch (cfg.wg_threads) {
-        case 128: return w3 ? launch_rs104_bs<128, 3>(a, cfg, stream) : launch_rs104_bs<128, 1>(a, cfg, stream);
-        case 512: return w3 ? launch_rs104_bs<512, 3>(a, cfg, stream) : launch_rs104_bs<512, 1>(a, cfg, stream);
-        default: return w3 ? launch_rs104_bs<256, 3>(a, cfg, stream) : launch_rs104_bs<256, 1>(a, cfg, stream);
+        case 128: return launch_rs104_bs<128>(a, cfg, stream);
+        case 512: return launch_rs104_bs<512>(a, cfg, stream);
+        default: return launch_rs104_bs<256>(a, cfg, stream);
     }
 }
 
@@ -727,13 +625,8 @@ static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t str
 
 const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
     if (cfg.mode == 1) return "rs104_kernel<DEC=false, XORONLY=true> (diagnostic)";
-    if (cfg.bitslice && len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0) {
-        switch (cfg.bitslice) {
-            case 1: return "rs104_bs_encode_kernel (bit-sliced)";
-            case 2: return "rs104_bs_encode_kernel (bit-sliced, >= 3 waves/SIMD)";
-            default: return "rs104_bs_pipe_kernel (bit-sliced, LDS-DMA pipelined)";
-        }
-    }
+    if (cfg.bitslice && len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0)
+        return "rs104_bs_encode_kernel (bit-sliced)";
     if (cfg.vec_per_thread == 2 && len % 8192 == 0) return "rs104_pair_kernel<DEC=false> (table lookup)";
     return "rs104_kernel<DEC=false> (table lookup)";
 }

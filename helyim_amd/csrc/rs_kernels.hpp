@@ -89,9 +89,8 @@ struct LaunchConfig {
     int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
     int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
-                                 // bytes: 1 = bit-sliced XOR program (default), 2 = same at >= 3
-                                 // waves/SIMD, 3/4 = LDS-DMA pipelined (window / contiguous order),
-                                 // 0 = table-lookup multiply (speed only)
+                                 // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
+                                 // multiply (speed only)
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees

@@ -342,10 +342,8 @@ int hec_set_workgroup_size(int threads);
 /* RS(10,4) encode kernel on shard lengths that are a multiple of
  * 32 x workgroup size bytes (8 KiB at 256 threads): 1 = bit-sliced (bytes
  * transposed into bit planes, the fixed parity matrix applied as a generated
- * XOR program; the default), 2 = the same compiled for >= 3 waves per SIMD,
- * 3 / 4 = the same software-pipelined through LDS-DMA (persistent grid,
- * window / contiguous chunk order), 0 = table-lookup GF multiply. All give
- * identical parity (parity-tested); speed only. */
+ * XOR program; the default), 0 = table-lookup GF multiply. Both give identical
+ * parity (parity-tested); speed only. Returns HEC_OK. */
 int hec_set_encode_kernel(int kind);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with

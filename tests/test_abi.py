@@ -135,9 +135,7 @@ def test_kernel_selection_knobs_host_only():
         assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_kernel<DEC=false>")
         assert lib.hec_set_encode_kernel(0) == 0
         assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_kernel<DEC=false>")
-        assert lib.hec_set_encode_kernel(3) == 0
-        assert "pipelined" in lib.hec_encode_kernel_name(1 << 20).decode()
-        assert lib.hec_set_encode_kernel(5) != 0
+        assert lib.hec_set_encode_kernel(2) != 0
         assert lib.hec_set_workgroup_size(128) == 0
         assert lib.hec_set_encode_kernel(1) == 0
         assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_bs_encode_kernel")  # 32 x 128 B

@@ -235,12 +235,11 @@ def test_pair_kernel_identical(gpu, remap, bpc):
         B.set_launch_config()
 
 
-@pytest.mark.parametrize("kind,wg,remap,bpc", [(0, 256, 1, 0), (1, 256, 1, 0), (1, 256, 0, 2), (1, 128, 1, 3), (2, 256, 1, 0),
-                                               (2, 512, 1, 0), (3, 256, 1, 0), (3, 128, 0, 1), (4, 256, 1, 0),
-                                               (4, 128, 1, 2)])
+@pytest.mark.parametrize("kind,wg,remap,bpc", [(0, 256, 1, 0), (1, 256, 1, 0), (1, 256, 0, 2), (1, 128, 1, 3),
+                                               (1, 128, 0, 0), (1, 512, 1, 0)])
 def test_bitslice_encode_matches_oracle(gpu, kind, wg, remap, bpc):
-    """The encode kernels (hec_set_encode_kernel 0: table lookup; 1..4 bit-sliced: plain,
-    >= 3 waves/SIMD, LDS-DMA pipelined in window / contiguous order) against
+    """The encode kernels (hec_set_encode_kernel 0: table lookup; 1: bit-sliced,
+    at 128 / 256 / 512 threads) against
     the C oracle: lengths that are a multiple of 32 x workgroup size take them,
     others fall back to the table kernel; in-place [S][14][L] and separate
     data/parity buffers."""

@@ -87,7 +87,7 @@ def main():
         enc, dec = np.array(res[c]["enc"]), np.array(res[c]["dec"])
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "pad": args.pad, "tile": args.tile,
                           "mode": ["gf", "xor_ceiling"][c[0]], "vec_per_thread": c[1], "max_blocks": c[2],
-                          "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7], "encode_kernel": ["table", "bitslice", "bitslice_w3", "bs_pipe_window", "bs_pipe_contig"][c[8]],
+                          "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7], "encode_kernel": ["table", "bitslice"][c[8]],
                           "enc_ms_med": round(float(np.median(enc)), 3), "enc_ms_min": round(float(enc.min()), 3),
                           "enc_GBps": round(nbytes / np.median(enc) / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 3),

@@ -273,7 +273,8 @@ int read_ranges(const std::string& base, const Shards& sh, uint64_t large, uint6
         },
         [&](size_t j, int shard, const uint8_t* src) {
             if (shard == lost[j].shard) std::memcpy(lost[j].dst, src, lost[j].size);
-        });
+        },
+        /*io_bound_fill=*/true);
 }
 
 int read_ranges(const std::string& base, uint64_t large, uint64_t small, const uint64_t* offsets,

@@ -107,7 +107,8 @@ uint64_t& host_staging_max();
 // length len and present mask; the decode reads its first 10 present shards,
 // which fill(j, slot, shard, dst) writes (len bytes) straight into staging
 // (non-zero return = that status aborts the call); take(j, shard, src) then
-// receives every erased shard. fill / take run on up to 16 threads.
+// receives every erased shard. fill / take run on up to 16 threads
+// (io_bound_fill: fill does preads, worth threads at smaller sizes).
 struct CompactJob {
     uint64_t len;
     uint32_t mask;
@@ -115,7 +116,7 @@ struct CompactJob {
 using CompactFill = std::function<int(size_t job, int slot, int shard, uint8_t* dst)>;
 using CompactTake = std::function<void(size_t job, int shard, const uint8_t* src)>;
 int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& jobs, const CompactFill& fill,
-                            const CompactTake& take);
+                            const CompactTake& take, bool io_bound_fill = false);
 
 // Run fn(i) for i in [0, n) on the library's persistent host worker pool
 // (host memcpy of staging): up to 16 threads, at least 1 MiB of `bytes` per
@@ -124,6 +125,18 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
 // Concurrent callers do not wait for each other: a call that finds the pool
 // busy runs serially on its own thread.
 void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>& fn);
+
+// Same pool for I/O-bound tasks (pread / fill callbacks): syscalls gain from
+// threads at smaller sizes than memcpy, so >= 128 KiB per thread.
+template <typename F>
+void parallel_io_for(size_t n, uint64_t bytes, F fn) {
+    const unsigned nt = unsigned(std::min<uint64_t>(16, bytes >> 17));
+    if (nt <= 1 || n < 2) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    pool_run(n, nt, std::function<void(size_t)>(fn));
+}
 
 template <typename F>
 void parallel_for(size_t n, uint64_t bytes, F fn) {

@@ -68,7 +68,7 @@ int ragged_scratch(RaggedScratch** out) {
 }  // namespace
 
 int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& jobs, const CompactFill& fill,
-                            const CompactTake& take) {
+                            const CompactTake& take, bool io_bound_fill) {
     const int k = rs->k, n = rs->n;
     struct Lay {
         uint64_t Lp, off, out_off;
@@ -108,19 +108,29 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     if ((rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
     // survivors the decode reads (the first k present shards) -> slots 0..k-1
     std::atomic<int> first_err{HEC_OK};
-    parallel_for(jobs.size(), in_total, [&](size_t j) {
+    // one task per (job, slot): a single large interval's 10 survivor reads run
+    // in parallel too
+    auto fill_one = [&](size_t t) {
+        const size_t j = t / size_t(k);
+        const int want = int(t % size_t(k));
         int used = 0;
-        for (int i = 0; i < n && used < k; ++i)
+        for (int i = 0; i < n; ++i)
             if ((jobs[j].mask >> i) & 1) {
-                const int r = fill(j, used, i, sc->host + lay[j].off + used * lay[j].Lp);
-                if (r) {
-                    int expect = HEC_OK;
-                    first_err.compare_exchange_strong(expect, r);
+                if (used == want) {
+                    const int r = fill(j, used, i, sc->host + lay[j].off + used * lay[j].Lp);
+                    if (r) {
+                        int expect = HEC_OK;
+                        first_err.compare_exchange_strong(expect, r);
+                    }
                     return;
                 }
                 ++used;
             }
-    });
+    };
+    if (io_bound_fill)
+        parallel_io_for(jobs.size() * size_t(k), in_total, fill_one);
+    else
+        parallel_for(jobs.size() * size_t(k), in_total, fill_one);
     if (first_err.load()) return first_err.load();
     std::memcpy(sc->hmeta, items.data(), items_bytes);
     const size_t map_off = (items_bytes + 255) / 256 * 256;

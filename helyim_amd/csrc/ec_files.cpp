@@ -39,8 +39,14 @@ namespace hec {
 namespace {
 
 constexpr int K = 10, M = 4, N = 14;
-constexpr int kSlots = 3;
-constexpr uint64_t kBatchBytes = 256ull << 20;  // data bytes per GPU job
+#ifndef HEC_FILE_SLOTS
+#define HEC_FILE_SLOTS 3
+#endif
+#ifndef HEC_FILE_BATCH_MIB
+#define HEC_FILE_BATCH_MIB 256
+#endif
+constexpr int kSlots = HEC_FILE_SLOTS;                                  // pipeline depth (build-time, measurement)
+constexpr uint64_t kBatchBytes = uint64_t(HEC_FILE_BATCH_MIB) << 20;  // data bytes per GPU job
 constexpr uint64_t kLargeSlice = 16ull << 20;   // per-shard slice of a large row
 constexpr int kIoThreads = 16;
 

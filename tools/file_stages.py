@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=12.0)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--fresh", action="store_true", help="delete the shard files before each timed encode")
     args = ap.parse_args()
     import helyim_amd as H
     from tools.bench_files import make_volume
@@ -28,8 +29,12 @@ def main():
         base = os.path.join(d, "v")
         nbytes = int(args.gib * 2**30)
         make_volume(base + ".dat", nbytes)
-        out = {"dat_bytes": nbytes, "encode_s": [], "rebuild_s": []}
+        out = {"dat_bytes": nbytes, "fresh": args.fresh, "encode_s": [], "rebuild_s": []}
+        H.write_ec_files(base)  # warm-up: device tables, pinned staging
         for _ in range(args.reps):
+            if args.fresh:
+                for i in range(14):
+                    os.remove(base + H.to_ext(i))
             t0 = time.perf_counter()
             H.write_ec_files(base)
             out["encode_s"].append(round(time.perf_counter() - t0, 4))

@@ -24,7 +24,27 @@ struct Pipeline {
     uint32_t* mask_dev[kDepth] = {};
     uint32_t* mask_host[kDepth] = {};  // pinned staging for per-chunk masks
     size_t slot_cap = 0, mask_cap = 0;
+    // pinned staging for pageable callers: two slots the kernels code in place
+    uint8_t* hslot[2] = {};
+    hipEvent_t hdone[2] = {};
+    size_t hslot_cap = 0;
+    int reserve_host(size_t bytes) {
+        if (!hdone[0])
+            for (auto& e : hdone) HEC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (bytes <= hslot_cap) return HEC_OK;
+        for (auto& h : hslot) {
+            if (h) HEC_HIP(hipHostFree(h));
+            h = nullptr;
+        }
+        hslot_cap = 0;
+        for (auto& h : hslot) HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault));
+        hslot_cap = bytes;
+        return HEC_OK;
+    }
     ~Pipeline() {
+        for (auto& h : hslot) (void)hipHostFree(h);
+        for (auto& e : hdone)
+            if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < kDepth; ++i) {
             (void)hipFree(slot[i]);
             (void)hipFree(mask_dev[i]);
@@ -156,8 +176,51 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
     }
     const uint64_t Lp = (shard_len + 255) / 256 * 256;  // device shard pitch
     const uint32_t C = chunk_stripes(Lp, rs->n, n_stripes);
-    if ((rc = p->reserve(size_t(C) * rs->n * Lp, 1))) return rc;
     const uint64_t dstripe = uint64_t(rs->n) * Lp;
+    if (zero_copy_enabled()) {
+        // Pageable memory: chunks are copied into two pinned slots on the host
+        // pool and coded in place by the zero-copy kernel; packing chunk i+1
+        // and unpacking chunk i-1 overlap the kernel of chunk i.
+        if ((rc = p->reserve(0, 1)) || (rc = p->reserve_host(size_t(C) * dstripe))) return rc;
+        uint8_t* zs[2] = {pinned_device_ptr(p->hslot[0]), pinned_device_ptr(p->hslot[1])};
+        if (zs[0] && zs[1]) {
+            hipStream_t st = p->streams[0];
+            auto unpack = [&](uint32_t s0, uint32_t c, int q) {
+                parallel_for(size_t(c) * m, uint64_t(c) * m * shard_len, [&](size_t t) {
+                    const uint32_t s = uint32_t(t / m);
+                    const int j = int(t % m);
+                    std::memcpy(h_parity + (s0 + s) * parity_stripe_stride + j * parity_shard_stride,
+                                p->hslot[q] + s * dstripe + uint64_t(k + j) * Lp, shard_len);
+                });
+            };
+            uint32_t prev_s0 = 0, prev_c = 0;
+            for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
+                const uint32_t c = std::min(C, n_stripes - s0);
+                const int q = int(it % 2);
+                uint8_t* h = p->hslot[q];
+                parallel_for(size_t(c) * k, uint64_t(c) * k * shard_len, [&](size_t t) {
+                    const uint32_t s = uint32_t(t / k);
+                    const int i = int(t % k);
+                    std::memcpy(h + s * dstripe + uint64_t(i) * Lp,
+                                h_data + (s0 + s) * data_stripe_stride + i * data_shard_stride, shard_len);
+                });
+                if ((rc = run_apply(gd->encode, uint32_t(k), zs[q], dstripe, Lp, zs[q] + uint64_t(k) * Lp, dstripe,
+                                    Lp, (shard_len + 15) / 16 * 16, c, nullptr, nullptr, st)))
+                    return rc;
+                HEC_HIP(hipEventRecord(p->hdone[q], st));
+                if (it > 0) {  // chunk it-1 (other slot) is done or nearly: hand its parity back
+                    HEC_HIP(hipEventSynchronize(p->hdone[1 - q]));
+                    unpack(prev_s0, prev_c, 1 - q);
+                }
+                prev_s0 = s0, prev_c = c;
+            }
+            const int last = int(((n_stripes + C - 1) / C - 1) % 2);
+            HEC_HIP(hipEventSynchronize(p->hdone[last]));
+            unpack(prev_s0, prev_c, last);
+            return HEC_OK;
+        }
+    }
+    if ((rc = p->reserve(size_t(C) * rs->n * Lp, 1))) return rc;
     for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
         const uint32_t c = std::min(C, n_stripes - s0);
         const int q = int(it % kDepth);
@@ -216,9 +279,68 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
     }
     const uint64_t Lp = (shard_len + 255) / 256 * 256;
     const uint32_t C = chunk_stripes(Lp, n, n_stripes);
+    const uint64_t dstripe = uint64_t(n) * Lp;
+    if (zero_copy_enabled()) {
+        // Pageable memory: the first k present shards of each stripe are copied
+        // into two pinned slots on the host pool, decoded in place there by the
+        // zero-copy kernel, and only the erased shards are copied back; chunk
+        // i+1's copies in and chunk i-1's copies out overlap chunk i's kernel.
+        if ((rc = p->reserve(0, C)) || (rc = p->reserve_host(size_t(C) * dstripe))) return rc;
+        if ((rc = ensure_dense_decode(rs, gd, p->streams[0]))) return rc;
+        uint8_t* zs[2] = {pinned_device_ptr(p->hslot[0]), pinned_device_ptr(p->hslot[1])};
+        uint32_t* zm[2] = {reinterpret_cast<uint32_t*>(pinned_device_ptr(p->mask_host[0])),
+                           reinterpret_cast<uint32_t*>(pinned_device_ptr(p->mask_host[1]))};
+        if (zs[0] && zs[1] && zm[0] && zm[1]) {
+            hipStream_t st = p->streams[0];
+            uint32_t bad = 0;
+            auto unpack = [&](uint32_t s0, uint32_t c, int q) {
+                parallel_for(size_t(c) * n, uint64_t(c) * 4 * shard_len, [&](size_t t) {
+                    const uint32_t s = uint32_t(t / n);
+                    const int i = int(t % n);
+                    const uint32_t mask = p->mask_host[q][s];
+                    if (__builtin_popcount(mask) < k || ((mask >> i) & 1)) return;
+                    std::memcpy(h_shards + (s0 + s) * stripe_stride + uint64_t(i) * shard_stride,
+                                p->hslot[q] + s * dstripe + uint64_t(i) * Lp, shard_len);
+                });
+            };
+            uint32_t prev_s0 = 0, prev_c = 0;
+            for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
+                const uint32_t c = std::min(C, n_stripes - s0);
+                const int q = int(it % 2);
+                for (uint32_t s = 0; s < c; ++s) {
+                    const uint32_t mask = h_present_masks[s0 + s] & full;
+                    p->mask_host[q][s] = mask;
+                    bad += __builtin_popcount(mask) < k ? 1u : 0u;
+                }
+                uint8_t* h = p->hslot[q];
+                parallel_for(size_t(c) * n, uint64_t(c) * k * shard_len, [&](size_t t) {
+                    const uint32_t s = uint32_t(t / n);
+                    const int i = int(t % n);
+                    const uint32_t mask = p->mask_host[q][s];
+                    if (__builtin_popcount(mask) < k || __builtin_popcount(mask) == n || !((mask >> i) & 1)) return;
+                    if (__builtin_popcount(mask & ((1u << i) - 1)) >= k) return;  // only the first k present
+                    std::memcpy(h + s * dstripe + uint64_t(i) * Lp,
+                                h_shards + (s0 + s) * stripe_stride + uint64_t(i) * shard_stride, shard_len);
+                });
+                if ((rc = run_apply(gd->decode_dense, uint32_t(k), zs[q], dstripe, Lp, zs[q], dstripe, Lp,
+                                    (shard_len + 15) / 16 * 16, c, zm[q], nullptr, st)))
+                    return rc;
+                HEC_HIP(hipEventRecord(p->hdone[q], st));
+                if (it > 0) {
+                    HEC_HIP(hipEventSynchronize(p->hdone[1 - q]));
+                    unpack(prev_s0, prev_c, 1 - q);
+                }
+                prev_s0 = s0, prev_c = c;
+            }
+            const int last = int(((n_stripes + C - 1) / C - 1) % 2);
+            HEC_HIP(hipEventSynchronize(p->hdone[last]));
+            unpack(prev_s0, prev_c, last);
+            if (n_bad_stripes) *n_bad_stripes = bad;
+            return HEC_OK;
+        }
+    }
     if ((rc = p->reserve(size_t(C) * n * Lp, C))) return rc;
     if ((rc = ensure_dense_decode(rs, gd, p->streams[0]))) return rc;
-    const uint64_t dstripe = uint64_t(n) * Lp;
     uint32_t bad = 0;
     for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
         const uint32_t c = std::min(C, n_stripes - s0);

@@ -34,7 +34,8 @@ def _host_stripes(S, L, pin=True):
 
 
 @pytest.mark.parametrize("L,S,pin", [(1, 3, True), (17, 5, True), (4096, 7, True), (65536 + 5, 9, True),
-                                     (1 << 20, 40, True), (1000, 4, False)])
+                                     (1 << 20, 40, True), (1000, 4, False), (1 << 20, 40, False),
+                                     (65536 + 5, 300, False)])
 def test_host_encode_batch(gpu, L, S, pin):
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -46,13 +47,14 @@ def test_host_encode_batch(gpu, L, S, pin):
     assert np.array_equal(a[:, 10:], ref)
 
 
-def test_host_reconstruct_every_pattern(gpu):
+@pytest.mark.parametrize("pin", [True, False])
+def test_host_reconstruct_every_pattern(gpu, pin):
     import helyim_amd as H
     import helyim_amd.batch as B
     rs = H.ReedSolomon(10, 4)
     pats = [c for e in range(0, 6) for c in itertools.combinations(range(14), e)]
     S, L = len(pats), 512 + 3
-    t = _host_stripes(S, L)
+    t = _host_stripes(S, L, pin)
     B.host_encode_batch(rs, t)
     good = t.clone()
     a = t.numpy()

@@ -29,9 +29,22 @@ def main():
     def enc():
         assert lib.hec_host_encode_batch(rs.handle, p, 14 * L, L, p + 10 * L, 14 * L, L, L, S) == 0
 
-    enc()
+    rng = np.random.default_rng(1)
+    masks = np.array([((1 << 14) - 1) & ~int(sum(1 << int(i) for i in rng.choice(14, 4, replace=False)))
+                      for _ in range(S)], dtype=np.uint32)
+
+    def dec():
+        assert lib.hec_host_reconstruct_batch(rs.handle, p, 14 * L, L, L, S, masks.ctypes.data, None) == 0
+
     res = {}
-    t0 = time.perf_counter(); enc(); res["pageable_copy_pipeline_s"] = time.perf_counter() - t0
+    for zc, name in ((1, "pooled_pinned_staging"), (0, "runtime_copies")):
+        lib.hec_set_host_zero_copy(zc)
+        enc()
+        dec()
+        t0 = time.perf_counter(); enc(); res[f"pageable_encode_{name}_s"] = time.perf_counter() - t0
+        t0 = time.perf_counter(); dec(); res[f"pageable_decode_{name}_s"] = time.perf_counter() - t0
+    lib.hec_set_host_zero_copy(1)
+    res["pageable_copy_pipeline_s"] = res["pageable_encode_pooled_pinned_staging_s"]
     for it in range(2):
         t0 = time.perf_counter()
         assert hip.hipHostRegister(ctypes.c_void_p(p), ctypes.c_size_t(a.nbytes), 0) == 0
@@ -45,7 +58,9 @@ def main():
             res["first_register_s"] = t1 - t0
     data = S * 10 * L
     out = {k: round(v, 6) for k, v in res.items()}
-    out["pageable_GiB_s"] = round(data / res["pageable_copy_pipeline_s"] / 2**30, 2)
+    for k in list(res):
+        if k.startswith("pageable_e") or k.startswith("pageable_d"):
+            out[k[:-2] + "_GiB_s"] = round(data / res[k] / 2**30, 2)
     out["register_encode_unregister_GiB_s"] = round(
         data / (res["first_register_s"] + res["zero_copy_encode_s"] + res["unregister_s"]) / 2**30, 2)
     ref = corc.encode_stripes(np.ascontiguousarray(a[:, :10]))

@@ -155,8 +155,10 @@ int hec_gpu_reconstruct_batch(const hec_rs_t* rs, uint8_t* d_shards, uint64_t st
  * Same strided layout as above but on HOST pointers; synchronous on return.
  * Pinned buffers the GPU can address (hipHostMalloc, torch pin_memory) are
  * coded zero-copy: the kernel reads and writes them over PCIe directly.
- * Other memory (pageable) is pipelined H2D -> kernel -> D2H over 3 HIP
- * streams so the copies overlap the kernels. */
+ * Pageable memory is copied chunk by chunk (host worker pool) into pinned
+ * slots that the kernel codes in place, the copies of one chunk overlapping
+ * the kernel of the next. With hec_set_host_zero_copy(0) both go through
+ * H2D -> kernel -> D2H over 3 HIP streams. */
 int hec_host_encode_batch(const hec_rs_t* rs,
                           const uint8_t* h_data, uint64_t data_stripe_stride, uint64_t data_shard_stride,
                           uint8_t* h_parity, uint64_t parity_stripe_stride, uint64_t parity_shard_stride,

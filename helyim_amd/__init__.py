@@ -23,7 +23,7 @@ from .ec import (  # noqa: F401
     DATA_SHARDS_COUNT, ERASURE_CODING_LARGE_BLOCK_SIZE, ERASURE_CODING_SMALL_BLOCK_SIZE,
     PARITY_SHARDS_COUNT, TOTAL_SHARDS_COUNT, EcVolume, Interval, find_data_filesize, find_needle_from_ecx, locate_data,
     read_ec_data, read_ec_needle, read_ec_needles, generate_ec_files, rebuild_ec_files,
-    rebuild_ecx_file, save_volume_info, to_ext, volume_ec_shards_generate, volume_ec_shards_rebuild,
+    rebuild_ecx_file, save_volume_info, to_ext, ec_shard_filename, ec_shard_base_filename, volume_ec_shards_generate, volume_ec_shards_rebuild,
     write_data_file, write_ec_files, write_index_file_from_ec_index, write_sorted_file_from_index,
 )
 

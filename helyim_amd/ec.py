@@ -27,6 +27,17 @@ def to_ext(ec_idx: int) -> str:
     return ".ec%02d" % ec_idx
 
 
+def ec_shard_filename(collection: str, dir: str, volume_id: int) -> str:
+    """Base path of a volume's shard files (shard.rs:51-57): ``dir/vid`` or
+    ``dir/collection_vid``; append ``to_ext(shard_id)`` for one shard."""
+    return "%s/%d" % (dir, volume_id) if not collection else "%s/%s_%d" % (dir, collection, volume_id)
+
+
+def ec_shard_base_filename(collection: str, volume_id: int) -> str:
+    """Directory-less base name (shard.rs:59-65)."""
+    return "%d" % volume_id if not collection else "%s_%d" % (collection, volume_id)
+
+
 def write_ec_files(base_filename: str) -> None:
     """base.dat -> base.ec00 .. base.ec13 (encoder.rs:39-46)."""
     check_ec(lib.hec_write_ec_files(base_filename.encode()))

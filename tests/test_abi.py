@@ -101,6 +101,12 @@ def test_constants_and_ext():
     assert H.ERASURE_CODING_LARGE_BLOCK_SIZE == 1 << 30
     assert H.ERASURE_CODING_SMALL_BLOCK_SIZE == 1 << 20
     assert [H.to_ext(i) for i in (0, 9, 13)] == [".ec00", ".ec09", ".ec13"]
+    # shard.rs:51-65 naming
+    assert H.ec_shard_filename("", "/data", 7) == "/data/7"
+    assert H.ec_shard_filename("pics", "/data", 7) == "/data/pics_7"
+    assert H.ec_shard_base_filename("", 42) == "42"
+    assert H.ec_shard_base_filename("pics", 42) == "pics_42"
+    assert H.ec_shard_filename("c", "d", 3) + H.to_ext(13) == "d/c_3.ec13"
 
 
 def test_file_layer_io_errors(tmp_path):

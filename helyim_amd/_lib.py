@@ -93,6 +93,9 @@ SIGNATURES = {
     "hec_set_xcd_parts": (_I, [_I]),
     "hec_set_chunk_rotation": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
+    "hec_device_count": (_I, [ctypes.POINTER(_I)]),
+    "hec_set_device": (_I, [_I]),
+    "hec_get_device": (_I, [ctypes.POINTER(_I)]),
     "hec_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
 }
 

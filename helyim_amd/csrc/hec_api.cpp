@@ -561,6 +561,33 @@ const char* hec_last_error_detail(void) { return g_detail.c_str(); }
 
 const char* hec_version(void) { return "libhec 0.1.0 (gfx950)"; }
 
+int hec_device_count(int* count) {
+    if (!count) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    *count = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return fail(HEC_ERR_NO_DEVICE, "no HIP device visible (libhec has no CPU fallback)");
+    }
+    *count = n;
+    return HEC_OK;
+}
+
+int hec_set_device(int device) {
+    int n;
+    int rc = hec_device_count(&n);
+    if (rc) return rc;
+    if (device < 0 || device >= n)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "device " + std::to_string(device) + " of " + std::to_string(n));
+    HEC_HIP(hipSetDevice(device));
+    return HEC_OK;
+}
+
+int hec_get_device(int* device) {
+    if (!device) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    return current_device(device);
+}
+
 const char* hec_encode_kernel_name(uint64_t shard_len) { return encode_kernel_name(shard_len, launch_config()); }
 
 int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, int blocks_per_cu) {

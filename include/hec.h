@@ -70,6 +70,16 @@ const char* hec_strerror(int status);
  * the two sizes of UnexpectedEcShardSize). Empty string when none. */
 const char* hec_last_error_detail(void);
 
+/* ---- device selection (no reference counterpart: helyim has no GPU) -------
+ * Every entry point works on the calling thread's current HIP device. A
+ * multi-GPU volume server that does not link HIP itself picks the device per
+ * call with these, e.g. volume_id % count before hec_write_ec_files (whole
+ * volumes per GPU); per-device state is independent, so calls
+ * on different devices run concurrently. */
+int hec_device_count(int* count);  /* HEC_ERR_NO_DEVICE (and 0) without a GPU */
+int hec_set_device(int device);    /* this thread only; HEC_ERR_INVALID_ARGUMENT if out of range */
+int hec_get_device(int* device);
+
 /* ---- geometry constants (helyim-ec/src/lib.rs:46-50) ---------------------- */
 #define HEC_DATA_SHARDS_COUNT 10u
 #define HEC_PARITY_SHARDS_COUNT 4u

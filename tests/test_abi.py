@@ -93,6 +93,10 @@ def test_no_cpu_fallback():
     with pytest.raises(H.DeviceError) as ei:
         rs.encode(sh)
     assert ei.value.code == 65  # HEC_ERR_NO_DEVICE
+    for call in (H.device_count, H.get_device, lambda: H.set_device(0)):
+        with pytest.raises(H.DeviceError) as ei:
+            call()
+        assert ei.value.code == 65
 
 
 def test_constants_and_ext():

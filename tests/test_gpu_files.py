@@ -94,3 +94,44 @@ def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path):
     assert H.rebuild_ec_files(base) == [2, 11]
     for i in range(14):
         assert open(base + H.to_ext(i), "rb").read() == sh[i].tobytes()
+
+
+def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path):
+    """hec_set_device per thread (hec.h): volumes encoded and rebuilt
+    concurrently from several threads, round-robin over the visible devices
+    (all on device 0 on a one-GPU box), each byte-identical to the fixture."""
+    import threading
+    import helyim_amd as H
+    n = H.device_count()
+    assert n >= 1 and 0 <= H.get_device() < n
+    for bad in (n, -1):
+        with pytest.raises(H.DeviceError) as ei:
+            H.set_device(bad)
+        assert ei.value.code == 66  # HEC_ERR_INVALID_ARGUMENT
+    g = golden("volume_30mb.json")
+    vol = O.synthetic_volume(g["dat_bytes"]).tobytes()
+    bases = [str(tmp_path / str(v)) for v in range(4)]
+    for b in bases:
+        open(b + ".dat", "wb").write(vol)
+    errs, seen = [], {}
+
+    def work(v, b):
+        try:
+            H.set_device(v % n)
+            seen[v] = H.get_device()
+            H.write_ec_files(b)
+            for i in (1, 4, 11, 13):
+                os.remove(b + H.to_ext(i))
+            assert H.rebuild_ec_files(b) == [1, 4, 11, 13]
+        except BaseException as e:  # surfaced in the main thread
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(v, b)) for v, b in enumerate(bases)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert seen == {v: v % n for v in range(4)}
+    for b in bases:
+        assert [_sha(b + H.to_ext(i)) for i in range(14)] == g["shard_sha256"]

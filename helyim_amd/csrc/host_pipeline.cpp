@@ -287,10 +287,10 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
         // i+1's copies in and chunk i-1's copies out overlap chunk i's kernel.
         if ((rc = p->reserve(0, C)) || (rc = p->reserve_host(size_t(C) * dstripe))) return rc;
         if ((rc = ensure_dense_decode(rs, gd, p->streams[0]))) return rc;
-        uint8_t* zs[2] = {pinned_device_ptr(p->hslot[0]), pinned_device_ptr(p->hslot[1])};
+        uint8_t* hz[2] = {pinned_device_ptr(p->hslot[0]), pinned_device_ptr(p->hslot[1])};
         uint32_t* zm[2] = {reinterpret_cast<uint32_t*>(pinned_device_ptr(p->mask_host[0])),
                            reinterpret_cast<uint32_t*>(pinned_device_ptr(p->mask_host[1]))};
-        if (zs[0] && zs[1] && zm[0] && zm[1]) {
+        if (hz[0] && hz[1] && zm[0] && zm[1]) {
             hipStream_t st = p->streams[0];
             uint32_t bad = 0;
             auto unpack = [&](uint32_t s0, uint32_t c, int q) {
@@ -322,7 +322,7 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
                     std::memcpy(h + s * dstripe + uint64_t(i) * Lp,
                                 h_shards + (s0 + s) * stripe_stride + uint64_t(i) * shard_stride, shard_len);
                 });
-                if ((rc = run_apply(gd->decode_dense, uint32_t(k), zs[q], dstripe, Lp, zs[q], dstripe, Lp,
+                if ((rc = run_apply(gd->decode_dense, uint32_t(k), hz[q], dstripe, Lp, hz[q], dstripe, Lp,
                                     (shard_len + 15) / 16 * 16, c, zm[q], nullptr, st)))
                     return rc;
                 HEC_HIP(hipEventRecord(p->hdone[q], st));

@@ -15,6 +15,7 @@
 // k+1, the GPU work of job k and the writes of job k-1 overlap.
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/vfs.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -412,14 +413,24 @@ struct Rs104 {
 // returned future gates the pipeline's writes. FALLOC_FL_KEEP_SIZE leaves the
 // visible size to the writes, so a failed call leaves the bytes the reference
 // would. Speed only: the filesystem allocates each file in one call instead of
-// page by page inside the writes. Filesystems without fallocate are skipped
-// silently. HEC_NO_PREALLOC=1 turns it off (measurement).
+// block by block inside the writes (re-encoding a 4 GiB volume over its old
+// shards on the box's overlay filesystem: 0.16 s with, 0.54-0.78 s without).
+// Skipped on tmpfs, where fallocate zero-fills the page cache up front and
+// the writes then copy over it (12 GiB volume in /dev/shm: 0.37-0.40 s fresh
+// without, 0.47-0.65 s with; tools/ab_prealloc*.sh). Filesystems without
+// fallocate are skipped silently. HEC_NO_PREALLOC=1 turns it off (measurement).
 std::shared_future<void> preallocate_async(const int* fds, int n, uint64_t bytes) {
     static const bool disabled = std::getenv("HEC_NO_PREALLOC") != nullptr;
     if (disabled || bytes == 0) return {};
+    constexpr long kTmpfsMagic = 0x01021994;
     std::vector<int> v;
-    for (int i = 0; i < n; ++i)
-        if (fds[i] >= 0) v.push_back(fds[i]);
+    for (int i = 0; i < n; ++i) {
+        if (fds[i] < 0) continue;
+        struct statfs st;
+        if (::fstatfs(fds[i], &st) == 0 && long(st.f_type) == kTmpfsMagic) continue;
+        v.push_back(fds[i]);
+    }
+    if (v.empty()) return {};
     return std::async(std::launch::async, [v, bytes] {
                std::vector<std::thread> th;
                for (int fd : v) th.emplace_back([fd, bytes] { (void)::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, off_t(bytes)); });

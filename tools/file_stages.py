@@ -21,15 +21,16 @@ def main():
     ap.add_argument("--gib", type=float, default=12.0)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--fresh", action="store_true", help="delete the shard files before each timed encode")
+    ap.add_argument("--dir", default="/dev/shm", help="filesystem to run on (default tmpfs: page-cache rate)")
     args = ap.parse_args()
     import helyim_amd as H
     from tools.bench_files import make_volume
-    d = tempfile.mkdtemp(prefix="hec_stages_", dir="/dev/shm")
+    d = tempfile.mkdtemp(prefix="hec_stages_", dir=args.dir)
     try:
         base = os.path.join(d, "v")
         nbytes = int(args.gib * 2**30)
         make_volume(base + ".dat", nbytes)
-        out = {"dat_bytes": nbytes, "fresh": args.fresh, "encode_s": [], "rebuild_s": []}
+        out = {"dir": args.dir, "dat_bytes": nbytes, "fresh": args.fresh, "encode_s": [], "rebuild_s": []}
         H.write_ec_files(base)  # warm-up: device tables, pinned staging
         for _ in range(args.reps):
             if args.fresh:

@@ -22,11 +22,22 @@ def _stream_ptr(stream=None):
     return s.cuda_stream
 
 
-def _check_stripes(t: torch.Tensor, rs: ReedSolomon):
+def _check_device(t: torch.Tensor):
+    # libhec works on the calling thread's current device (hec.h): a tensor
+    # on another GPU would be addressed through the wrong device's page tables
+    if t.device.index != torch.cuda.current_device():
+        raise ValueError(f"tensor on {t.device}, current device is cuda:{torch.cuda.current_device()}")
+
+
+def _check_stripes(t: torch.Tensor, rs: ReedSolomon, shards: int = None):
     if t.dtype != torch.uint8 or not t.is_cuda or t.dim() != 3:
         raise TypeError("expected a uint8 CUDA tensor [stripes, shards, L]")
     if t.stride(2) != 1:
         raise ValueError("shard bytes must be contiguous")
+    want = rs.total_shard_count() if shards is None else shards
+    if t.shape[1] != want:
+        raise ValueError(f"expected {want} shards per stripe, got {t.shape[1]}")
+    _check_device(t)
 
 
 def encode_batch(rs: ReedSolomon, stripes: torch.Tensor, stream=None) -> None:
@@ -34,7 +45,6 @@ def encode_batch(rs: ReedSolomon, stripes: torch.Tensor, stream=None) -> None:
     _check_stripes(stripes, rs)
     k = rs.data_shard_count()
     S, n, L = stripes.shape
-    assert n == rs.total_shard_count()
     st, sh = stripes.stride(0), stripes.stride(1)
     base = stripes.data_ptr()
     check(lib.hec_gpu_encode_batch(rs.handle, base, st, sh, base + k * sh, st, sh, L, S,
@@ -43,7 +53,11 @@ def encode_batch(rs: ReedSolomon, stripes: torch.Tensor, stream=None) -> None:
 
 def encode_batch_sep(rs: ReedSolomon, data: torch.Tensor, parity: torch.Tensor, stream=None) -> None:
     """data[S, k, L] -> parity[S, m, L] (separate buffers)."""
+    _check_stripes(data, rs, rs.data_shard_count())
+    _check_stripes(parity, rs, rs.parity_shard_count())
     S, k, L = data.shape
+    if parity.shape[0] != S or parity.shape[2] != L:
+        raise ValueError(f"parity {tuple(parity.shape)} does not match data {tuple(data.shape)}")
     check(lib.hec_gpu_encode_batch(rs.handle, data.data_ptr(), data.stride(0), data.stride(1),
                                    parity.data_ptr(), parity.stride(0), parity.stride(1), L, S,
                                    _stream_ptr(stream)))
@@ -54,22 +68,32 @@ def reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks: tor
     """Rebuild erased shards in place; present_masks int32 [S] (bit i = shard i present)."""
     _check_stripes(stripes, rs)
     S, n, L = stripes.shape
-    assert present_masks.is_cuda and present_masks.dtype == torch.int32 and present_masks.numel() == S
+    if not (present_masks.is_cuda and present_masks.dtype == torch.int32 and present_masks.numel() == S
+            and present_masks.is_contiguous()):
+        raise ValueError("present_masks must be a contiguous int32 CUDA tensor with one word per stripe")
+    _check_device(present_masks)
+    if bad_stripes is not None:
+        if not (bad_stripes.is_cuda and bad_stripes.dtype in (torch.int32, torch.uint32)
+                and bad_stripes.numel() >= 1):
+            raise ValueError("bad_stripes must be a 32-bit CUDA tensor")
+        _check_device(bad_stripes)
     bad = bad_stripes.data_ptr() if bad_stripes is not None else None
     check(lib.hec_gpu_reconstruct_batch(rs.handle, stripes.data_ptr(), stripes.stride(0),
                                         stripes.stride(1), L, S, present_masks.data_ptr(), bad,
                                         _stream_ptr(stream)))
 
 
-def _check_host(t: torch.Tensor):
+def _check_host(t: torch.Tensor, rs: ReedSolomon):
     if t.dtype != torch.uint8 or t.is_cuda or t.dim() != 3 or t.stride(2) != 1:
         raise TypeError("expected a host uint8 tensor [stripes, shards, L] with contiguous shards")
+    if t.shape[1] != rs.total_shard_count():
+        raise ValueError(f"expected {rs.total_shard_count()} shards per stripe, got {t.shape[1]}")
 
 
 def host_encode_batch(rs: ReedSolomon, stripes: torch.Tensor) -> None:
     """Host-memory stripes[S, total, L] (pin_memory() for full PCIe rate):
     parity computed on the GPU, pipelined H2D -> kernel -> D2H."""
-    _check_host(stripes)
+    _check_host(stripes, rs)
     k = rs.data_shard_count()
     S, n, L = stripes.shape
     st, sh = stripes.stride(0), stripes.stride(1)
@@ -82,27 +106,44 @@ def host_reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks
     (fewer than data_shards present)."""
     import ctypes
     import numpy as np
-    _check_host(stripes)
+    _check_host(stripes, rs)
     S, n, L = stripes.shape
     m = np.ascontiguousarray(np.asarray(present_masks, dtype=np.uint32))
-    assert m.size == S
+    if m.size != S:
+        raise ValueError(f"{m.size} present masks for {S} stripes")
     bad = ctypes.c_uint32(0)
     check(lib.hec_host_reconstruct_batch(rs.handle, stripes.data_ptr(), stripes.stride(0), stripes.stride(1), L,
                                          S, m.ctypes.data, ctypes.byref(bad)))
     return int(bad.value)
 
 
-def _desc_array(descs):
-    """descs: iterable of (offset, shard_stride, shard_len, present_mask)."""
+def _desc_array(descs, base: torch.Tensor, shards: int):
+    """descs: iterable of (offset, shard_stride, shard_len, present_mask).
+    Every stripe's bytes [offset, offset + (shards-1)*stride + len) must lie
+    inside ``base`` (checked here: the C ABI only sees a pointer)."""
     import numpy as np
     dt = np.dtype([("offset", "<u8"), ("shard_stride", "<u8"), ("shard_len", "<u4"), ("present_mask", "<u4")])
-    return np.array([tuple(int(x) for x in d) for d in descs], dtype=dt)
+    d = np.array([tuple(int(x) for x in r) for r in descs], dtype=dt)
+    if base.dtype != torch.uint8 or not base.is_cuda or not base.is_contiguous():
+        raise TypeError("base must be a contiguous uint8 CUDA tensor")
+    _check_device(base)
+    if len(d):
+        off = d["offset"].astype(object)
+        end = off + (shards - 1) * d["shard_stride"].astype(object) + d["shard_len"].astype(object)
+        big = [i for i in range(len(d)) if end[i] > base.numel()
+               or (d["shard_len"][i] and d["shard_stride"][i] < d["shard_len"][i])]
+        if big:
+            i = big[0]
+            raise ValueError(f"stripe {i} (offset {int(d['offset'][i])}, stride {int(d['shard_stride'][i])}, "
+                             f"len {int(d['shard_len'][i])}) overlaps itself or runs past base "
+                             f"({base.numel()} bytes)")
+    return d
 
 
 def encode_ragged(rs: ReedSolomon, base: torch.Tensor, descs, stream=None) -> None:
     """RS(10,4) encode of stripes of mixed lengths in one launch; descs rows are
     (byte offset of shard 0 in base, shard stride, shard length, unused)."""
-    d = _desc_array(descs)
+    d = _desc_array(descs, base, rs.total_shard_count())
     check(lib.hec_gpu_encode_ragged(rs.handle, base.data_ptr(), d.ctypes.data, len(d), _stream_ptr(stream)))
 
 
@@ -110,7 +151,7 @@ def reconstruct_ragged(rs: ReedSolomon, base: torch.Tensor, descs, bad_stripes: 
                        stream=None) -> None:
     """Reconstruct stripes of mixed lengths and patterns in place, one launch;
     descs rows are (offset, shard stride, shard length, present mask)."""
-    d = _desc_array(descs)
+    d = _desc_array(descs, base, rs.total_shard_count())
     bad = bad_stripes.data_ptr() if bad_stripes is not None else None
     check(lib.hec_gpu_reconstruct_ragged(rs.handle, base.data_ptr(), d.ctypes.data, len(d), bad,
                                          _stream_ptr(stream)))
@@ -118,7 +159,13 @@ def reconstruct_ragged(rs: ReedSolomon, base: torch.Tensor, descs, bad_stripes: 
 
 def fill_splitmix(t: torch.Tensor, bytes_per_stripe: int, seed_base: int, stream=None) -> None:
     """Fill the first bytes_per_stripe bytes of each t[s] with splitmix64(seed_base + s)."""
+    if t.dtype != torch.uint8 or not t.is_cuda or t.dim() < 1:
+        raise TypeError("expected a uint8 CUDA tensor")
+    _check_device(t)
     S = t.shape[0]
+    room = t.untyped_storage().nbytes() - t.storage_offset()
+    if S and (bytes_per_stripe > t.stride(0) and S > 1 or (S - 1) * t.stride(0) + bytes_per_stripe > room):
+        raise ValueError(f"{S} rows of {bytes_per_stripe} bytes at pitch {t.stride(0)} do not fit the tensor")
     check(lib.hec_gpu_fill_splitmix(t.data_ptr(), t.stride(0), bytes_per_stripe, S, seed_base,
                                     _stream_ptr(stream)))
 

@@ -511,3 +511,30 @@ def test_full_config_every_4_erasure_pattern_and_linearity(gpu):
     B.encode_batch(rs, u)
     torch.cuda.synchronize()
     assert torch.equal(u[:, 10:], good_par ^ par_u)
+
+
+def test_batch_argument_checks_before_launch(gpu):
+    """The Python mirror rejects shapes the kernels would run past (the C ABI
+    only sees pointers), before anything is launched."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    t = torch.zeros((2, 14, 4096), dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        B.encode_batch(rs, t[:, :13])                       # 13 shards
+    with pytest.raises(ValueError):
+        B.encode_batch_sep(rs, t[:, :10], torch.zeros((2, 4, 1024), dtype=torch.uint8, device="cuda"))
+    with pytest.raises(ValueError):
+        B.reconstruct_batch(rs, t, torch.zeros(3, dtype=torch.int32, device="cuda"))
+    with pytest.raises(ValueError):
+        B.reconstruct_batch(rs, t, torch.zeros(2, dtype=torch.int64, device="cuda"))
+    base = torch.zeros(14 * 4096, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        B.encode_ragged(rs, base, [[1, 4096, 4096, 0]])        # last shard runs 1 byte past base
+    with pytest.raises(ValueError):
+        B.reconstruct_ragged(rs, base, [[0, 1024, 4096, 0x3FF]])  # shards overlap
+    with pytest.raises(ValueError):
+        B.fill_splitmix(t, 14 * 4096 + 1, 1)
+    B.encode_ragged(rs, base, [[0, 4096, 4096, 0]])            # exact fit is fine
+    torch.cuda.synchronize()

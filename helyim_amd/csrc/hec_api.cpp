@@ -702,9 +702,13 @@ int hec_gpu_encode_batch(const hec_rs_t* rs, const uint8_t* d_data, uint64_t dat
                          uint64_t parity_shard_stride, uint64_t shard_len, uint32_t n_stripes, void* stream) {
     if (!rs || !d_data || !d_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
     if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    int rc;
+    if ((rc = check_strided("data", uint32_t(rs->k), data_stripe_stride, data_shard_stride, shard_len, n_stripes)) ||
+        (rc = check_strided("parity", uint32_t(rs->m), parity_stripe_stride, parity_shard_stride, shard_len,
+                            n_stripes)))
+        return rc;
     GeomDevice* gd;
-    int rc = geom_device(rs, &gd);
-    if (rc) return rc;
+    if ((rc = geom_device(rs, &gd))) return rc;
     return run_apply(gd->encode, uint32_t(rs->k), d_data, data_stripe_stride, data_shard_stride, d_parity,
                      parity_stripe_stride, parity_shard_stride, shard_len, n_stripes, nullptr, nullptr,
                      static_cast<hipStream_t>(stream));
@@ -715,9 +719,10 @@ int hec_gpu_reconstruct_batch(const hec_rs_t* rs, uint8_t* d_shards, uint64_t st
                               uint32_t* d_bad_stripes, void* stream) {
     if (!rs || !d_shards || !d_present_masks) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
     if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    int rc;
+    if ((rc = check_strided("shards", uint32_t(rs->n), stripe_stride, shard_stride, shard_len, n_stripes))) return rc;
     GeomDevice* gd;
-    int rc = geom_device(rs, &gd);
-    if (rc) return rc;
+    if ((rc = geom_device(rs, &gd))) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if ((rc = ensure_dense_decode(rs, gd, s))) return rc;
     return run_apply(gd->decode_dense, uint32_t(rs->k), d_shards, stripe_stride, shard_stride, d_shards,

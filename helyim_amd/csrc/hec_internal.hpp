@@ -25,6 +25,23 @@ namespace hec {
 // Thread-local failure detail (hec_last_error_detail).
 void set_detail(const std::string& s);
 int fail(int code, const std::string& detail);
+
+// Strided-batch geometry sanity (the C ABI sees only pointers, so sizes cannot
+// be checked): shards of a stripe and stripes of a shard must not overlap,
+// and the batch's byte extent must not wrap the address space.
+inline int check_strided(const char* what, uint32_t shards, uint64_t stripe_stride, uint64_t shard_stride,
+                         uint64_t len, uint32_t n_stripes) {
+    if (shards > 1 && shard_stride < len)
+        return fail(HEC_ERR_INVALID_ARGUMENT, std::string(what) + ": shard stride below shard length");
+    if (n_stripes > 1 && stripe_stride < len)
+        return fail(HEC_ERR_INVALID_ARGUMENT, std::string(what) + ": stripe stride below shard length");
+    uint64_t a, b, e;
+    if (__builtin_mul_overflow(uint64_t(n_stripes ? n_stripes - 1 : 0), stripe_stride, &a) ||
+        __builtin_mul_overflow(uint64_t(shards ? shards - 1 : 0), shard_stride, &b) ||
+        __builtin_add_overflow(a, b, &e) || __builtin_add_overflow(e, len, &e))
+        return fail(HEC_ERR_INVALID_ARGUMENT, std::string(what) + ": batch extent overflows");
+    return HEC_OK;
+}
 int hip_fail(hipError_t e, const char* what);
 
 #define HEC_HIP(call)                                          \

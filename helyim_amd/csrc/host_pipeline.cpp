@@ -155,9 +155,13 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
     if (!rs || !h_data || !h_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
     if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
     if (n_stripes == 0) return HEC_OK;
+    int rc;
+    if ((rc = check_strided("data", uint32_t(rs->k), data_stripe_stride, data_shard_stride, shard_len, n_stripes)) ||
+        (rc = check_strided("parity", uint32_t(rs->m), parity_stripe_stride, parity_shard_stride, shard_len,
+                            n_stripes)))
+        return rc;
     GeomDevice* gd;
-    int rc = geom_device(rs, &gd);
-    if (rc) return rc;
+    if ((rc = geom_device(rs, &gd))) return rc;
     Pipeline* p;
     if ((rc = pipeline(&p))) return rc;
     std::lock_guard<std::mutex> lk(p->mu);
@@ -248,9 +252,10 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
     if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
     if (n_bad_stripes) *n_bad_stripes = 0;
     if (n_stripes == 0) return HEC_OK;
+    int rc;
+    if ((rc = check_strided("shards", uint32_t(rs->n), stripe_stride, shard_stride, shard_len, n_stripes))) return rc;
     GeomDevice* gd;
-    int rc = geom_device(rs, &gd);
-    if (rc) return rc;
+    if ((rc = geom_device(rs, &gd))) return rc;
     Pipeline* p;
     if ((rc = pipeline(&p))) return rc;
     std::lock_guard<std::mutex> lk(p->mu);

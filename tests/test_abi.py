@@ -158,3 +158,24 @@ def test_kernel_selection_knobs_host_only():
         lib.hec_set_kernel_mode(0)
         lib.hec_set_workgroup_size(256)
         lib.hec_set_encode_kernel(1)
+
+
+def test_strided_batch_geometry_checked_before_device():
+    """Overlapping shards/stripes and wrapping extents are refused by the C ABI
+    before any device work (fake non-null pointers are never touched)."""
+    import helyim_amd as H
+    lib, rs = H.lib, H.ReedSolomon(10, 4)
+    P, L = 0x1000, 4096
+    bad_encode = [
+        (P, 14 * L, L - 16, P, 14 * L, L, L, 2),          # data shards overlap
+        (P, 14 * L, L, P, 14 * L, L - 1, L, 2),           # parity shards overlap
+        (P, L - 1, 10 * L, P, L, 10 * L, L, 2),           # data stripes overlap
+        (P, 1 << 62, L, P, 14 * L, L, L, 8),              # extent wraps
+    ]
+    for args in bad_encode:
+        assert lib.hec_gpu_encode_batch(rs.handle, *args, None) == 66, args
+        assert lib.hec_host_encode_batch(rs.handle, *args) == 66, args
+    masks = (ctypes.c_uint32 * 2)(0x3FFF, 0x3FFF)
+    assert lib.hec_gpu_reconstruct_batch(rs.handle, P, 14 * L, L - 1, L, 2, P, None, None) == 66
+    assert lib.hec_host_reconstruct_batch(rs.handle, P, 14 * L, L - 1, L, 2, masks, None) == 66
+    assert lib.hec_host_reconstruct_batch(rs.handle, P, 1 << 63, L, L, 3, masks, None) == 66

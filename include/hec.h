@@ -144,7 +144,11 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
  * hipStream_t (NULL = default stream). Calls are asynchronous. */
 
 /* Encode n_stripes stripes: read data shards 0..data from d_data, write parity
- * shards 0..parity to d_parity (shard index relative to each base). */
+ * shards 0..parity to d_parity (shard index relative to each base).
+ * All strided batches (device and host) return HEC_ERR_INVALID_ARGUMENT,
+ * before any device work, when shards of a stripe overlap (shard stride <
+ * shard_len), stripes overlap (stripe stride < shard_len) or the batch's byte
+ * extent wraps 64 bits. Buffer sizes themselves cannot be checked here. */
 int hec_gpu_encode_batch(const hec_rs_t* rs,
                          const uint8_t* d_data, uint64_t data_stripe_stride, uint64_t data_shard_stride,
                          uint8_t* d_parity, uint64_t parity_stripe_stride, uint64_t parity_shard_stride,

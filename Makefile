@@ -7,7 +7,7 @@ SRC := $(wildcard helyim_amd/csrc/*.cpp) $(wildcard helyim_amd/csrc/*.hip)
 HDR := $(wildcard helyim_amd/csrc/*.hpp) $(wildcard helyim_amd/csrc/*.inc) include/hec.h
 OBJ := $(patsubst helyim_amd/csrc/%,build/obj/%.o,$(SRC))
 
-all: helyim_amd/libhec.so oracle
+all: helyim_amd/libhec.so oracle build/cabi_bench
 
 helyim_amd/libhec.so: $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -lpthread
@@ -22,6 +22,11 @@ build/obj/%.cpp.o: helyim_amd/csrc/%.cpp $(HDR)
 
 oracle:
 	$(MAKE) -C oracle
+
+# The BASELINE workload through the C ABI alone (no Python / PyTorch).
+build/cabi_bench: tools/cabi_bench.cpp include/hec.h helyim_amd/libhec.so
+	@mkdir -p build
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lhelyim_amd -lhec -Wl,-rpath,'$$ORIGIN/../helyim_amd'
 
 # Measurement variants of the kernel file (cache policy of shard streams).
 VARIANTS := ntl0_nts0 ntl0_nts1 ntl1_nts0

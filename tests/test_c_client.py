@@ -45,3 +45,19 @@ def test_c_client_parity(gpu, tmp_path):
     r = subprocess.run([exe, "gpu", str(tmp_path)], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "0 failed checks" in r.stdout
+
+
+@pytest.mark.gpu
+def test_c_abi_bench_small(gpu):
+    """tools/cabi_bench.cpp (built by `make all`): the bench workload through
+    the C ABI alone, at 64 stripes, must verify its sampled rebuilds."""
+    import json
+    exe = os.path.join(ROOT, "build", "cabi_bench")
+    if not os.path.exists(exe):
+        pytest.fail("build/cabi_bench not built (run make)")
+    env = dict(os.environ)
+    env.pop("HEC_LIB_PATH", None)
+    r = subprocess.run([exe, "64", "2", "1"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["verified"] is True and out["stripes"] == 64

@@ -6,4 +6,5 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 120 ./build/cabi_bench > $OUT/cabi_bench.json 2>&1
 bash tools/profile.sh $TAG

@@ -43,6 +43,14 @@ def test_small_geometry_vs_oracle(gpu, tmp_path, size):
     O.write_ec_files(b, buf, large, small)
     for i in range(14):
         assert open(a + H.to_ext(i), "rb").read() == open(b + O.to_ext(i), "rb").read(), i
+    # rebuild (1 MiB read rows, encoder.rs:244-307) of a seeded 1-4 shard drop
+    rng = np.random.default_rng(size)
+    drop = sorted(int(i) for i in rng.choice(14, int(rng.integers(1, 5)), replace=False))
+    want = [open(a + H.to_ext(i), "rb").read() for i in range(14)]
+    for i in drop:
+        os.remove(a + H.to_ext(i))
+    assert H.rebuild_ec_files(a) == drop
+    assert [open(a + H.to_ext(i), "rb").read() for i in range(14)] == want
 
 
 def test_unexpected_block_size(gpu, tmp_path):

@@ -17,6 +17,8 @@
 //  * Tables and shard ids are wave-uniform -> scalar loads (SGPRs); only the
 //    data is vector traffic: coalesced 16 B/lane loads and stores (1 KiB per
 //    wave instruction), non-temporal since every byte is touched once.
+#include <algorithm>
+
 #include "rs_kernels.hpp"
 #include "bitslice.hpp"
 
@@ -615,7 +617,7 @@ static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t str
     if (a.n_items == 0) return hipSuccess;
     uint64_t grid = a.n_items;
     if (cfg.max_blocks > 0 && grid > uint64_t(cfg.max_blocks)) grid = uint64_t(cfg.max_blocks);
-    if (grid > 0x7FFFFFFFull) grid = 0x7FFFFFFFull;
+    if (grid > kMaxLaunchBlocks) grid = kMaxLaunchBlocks;  // grid-stride covers the rest
     a.xcd_remap = cfg.xcd_remap ? 1u : 0u;
     // Occupancy cap: dynamic LDS that only blocks_per_cu workgroups fit in 160 KiB.
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
@@ -633,11 +635,28 @@ const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
 
 hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
                         hipStream_t stream) {
-    // RS(10,4) fast path: fixed 4-row table stride, one 4 KiB chunk per workgroup.
-    const uint64_t items = ((a.len + 4095) / 4096) * a.n_stripes;
+    // RS(10,4) fast path: fixed 4-row table stride, one chunk of >= 4 KiB per
+    // workgroup and no grid-stride loop, so one launch takes at most
+    // kMaxLaunchBlocks chunks: larger batches (tens of millions of short
+    // stripes) go in stripe ranges.
+    const uint64_t per_stripe = (a.len + 4095) / 4096;
+    const uint64_t items = per_stripe * a.n_stripes;
+    if (a.fast104 && items > kMaxLaunchBlocks && a.n_stripes > 1 && per_stripe <= kMaxLaunchBlocks) {
+        const uint32_t step = uint32_t(kMaxLaunchBlocks / per_stripe);
+        for (uint32_t s0 = 0; s0 < a.n_stripes; s0 += step) {
+            ApplyArgs b = a;
+            b.n_stripes = std::min(step, a.n_stripes - s0);
+            b.in_base += uint64_t(s0) * a.in_stripe;
+            b.out_base += uint64_t(s0) * a.out_stripe;
+            if (b.masks) b.masks += s0;
+            hipError_t e = launch_apply(b, nin, aligned, cfg, stream);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     const bool pair_ok = cfg.vec_per_thread == 2 && a.len % 8192 == 0;
     if (a.fast104 && aligned && (cfg.vec_per_thread == 1 || pair_ok) && cfg.max_blocks == 0 &&
-        items < 0x7FFFFFFFull) {
+        items <= kMaxLaunchBlocks) {
         if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, cfg, stream)
                                           : launch_rs104<true, false>(a, cfg, stream);
         if (cfg.bitslice && cfg.mode == 0 && a.len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0)

@@ -21,6 +21,10 @@ struct DevPlan {
 
 constexpr uint32_t kNoPlan = 0xFFFFFFFFu;   // mask LUT entry: too few shards present
 constexpr int kThreads = 256;               // 4 waves of 64 lanes
+// Workgroups per launch: the dispatch packet's grid is 32-bit in work-items,
+// so 2^23 workgroups (2^31 work-items at 256 threads, also at 1024 threads with
+// 4x larger chunks) keeps every launch legal.
+constexpr uint64_t kMaxLaunchBlocks = 1ull << 23;
 constexpr int kVecBytes = 16;               // one dwordx4 per lane per access
 
 struct ApplyArgs {

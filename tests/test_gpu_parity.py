@@ -538,3 +538,32 @@ def test_batch_argument_checks_before_launch(gpu):
         B.fill_splitmix(t, 14 * 4096 + 1, 1)
     B.encode_ragged(rs, base, [[0, 4096, 4096, 0]])            # exact fit is fine
     torch.cuda.synchronize()
+
+
+def test_batch_over_launch_limit_is_split(gpu):
+    """2^24 + 5 stripes of 16 B: more workgroups than one launch can carry
+    (a 256-thread grid of 2^24 workgroups is 2^32 work-items), so the batch
+    runs in stripe ranges of kMaxLaunchBlocks; stripes on both sides of every
+    range edge are checked against the oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = (1 << 24) + 5, 16
+    t = torch.empty((S, 14, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t, 10 * L, 0x5EED1000)
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    idx = torch.tensor([0, (1 << 23) - 1, 1 << 23, (1 << 24) - 1, 1 << 24, S - 1], device="cuda")
+    host = t[idx].cpu().numpy()
+    assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
+    masks = torch.full((S,), 0x3FFF & ~0b10000000100101, dtype=torch.int32, device="cuda")  # shards 0, 2, 5, 13
+    want = t[idx].clone()
+    for i in (0, 2, 5, 13):
+        t[:, i] = 0
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.reconstruct_batch(rs, t, masks, bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0
+    assert torch.equal(t[idx], want)
+    assert int(t[:, 13].sum(dtype=torch.int64).item()) > 0  # last range rebuilt too

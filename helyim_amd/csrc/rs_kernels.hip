@@ -505,18 +505,25 @@ __global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
 // Ragged encode with every stripe length a multiple of 8 KiB: workgroup ->
 // stripe map as rs104_ragged_kernel, one 8 KiB column range per workgroup.
 __global__ __launch_bounds__(kThreads) void rs104_bs_ragged_kernel(RaggedArgs a) {
-    const uint32_t s = as_const(a.block_item)[blockIdx.x];
+    const uint32_t blk = blockIdx.x + a.block_base;
+    const uint32_t s = as_const(a.block_item)[blk];
     const __attribute__((address_space(4))) RaggedItem* it = as_const(a.items) + s;
     const uint64_t off = it->off, stride = it->shard_stride;
     const uint32_t first = it->first_block;
     const uint8_t* b = a.base + off;
-    rs104_bs_chunk<kThreads>(b, a.base + off + 10 * stride, stride, stride, blockIdx.x - first);
+    rs104_bs_chunk<kThreads>(b, a.base + off + 10 * stride, stride, stride, blk - first);
 }
 
 hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
-    if (a.n_blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(rs104_bs_ragged_kernel, dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
-    return hipGetLastError();
+    for (uint64_t b0 = 0; b0 < a.n_blocks; b0 += kMaxLaunchBlocks) {  // see kMaxLaunchBlocks
+        RaggedArgs r = a;
+        r.block_base = uint32_t(b0);
+        const uint32_t nb = uint32_t(std::min<uint64_t>(kMaxLaunchBlocks, a.n_blocks - b0));
+        hipLaunchKernelGGL(rs104_bs_ragged_kernel, dim3(nb), dim3(kThreads), 0, stream, r);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 template <int TB>
@@ -547,25 +554,32 @@ static hipError_t launch_rs104_bs_cfg(const ApplyArgs& a, const LaunchConfig& cf
 // lays stripes out back to back and passes a workgroup -> stripe map.
 template <bool DEC, bool COMPACT>
 __global__ __launch_bounds__(kThreads) void rs104_ragged_kernel(RaggedArgs a) {
-    const uint32_t s = as_const(a.block_item)[blockIdx.x];
+    const uint32_t blk = blockIdx.x + a.block_base;
+    const uint32_t s = as_const(a.block_item)[blk];
     const __attribute__((address_space(4))) RaggedItem* it = as_const(a.items) + s;
     const uint64_t off = it->off, stride = it->shard_stride;
     const uint32_t len = it->len, mask = it->mask, first = it->first_block;
     uint8_t* b = a.base + off;
     uint8_t* o = COMPACT ? a.base + it->out_off : (DEC ? b : b + 10 * stride);
-    rs104_chunk<DEC, false, COMPACT>(b, o, stride, stride, len, blockIdx.x - first, mask, as_const(a.tabs),
+    rs104_chunk<DEC, false, COMPACT>(b, o, stride, stride, len, blk - first, mask, as_const(a.tabs),
                                      as_const(a.lut), a.bad_count);
 }
 
 hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream) {
-    if (a.n_blocks == 0) return hipSuccess;
-    if (decode && a.compact)
-        hipLaunchKernelGGL((rs104_ragged_kernel<true, true>), dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
-    else if (decode)
-        hipLaunchKernelGGL((rs104_ragged_kernel<true, false>), dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
-    else
-        hipLaunchKernelGGL((rs104_ragged_kernel<false, false>), dim3(a.n_blocks), dim3(kThreads), 0, stream, a);
-    return hipGetLastError();
+    for (uint64_t b0 = 0; b0 < a.n_blocks; b0 += kMaxLaunchBlocks) {  // see kMaxLaunchBlocks
+        RaggedArgs r = a;
+        r.block_base = uint32_t(b0);
+        const dim3 grid(uint32_t(std::min<uint64_t>(kMaxLaunchBlocks, a.n_blocks - b0)));
+        if (decode && a.compact)
+            hipLaunchKernelGGL((rs104_ragged_kernel<true, true>), grid, dim3(kThreads), 0, stream, r);
+        else if (decode)
+            hipLaunchKernelGGL((rs104_ragged_kernel<true, false>), grid, dim3(kThreads), 0, stream, r);
+        else
+            hipLaunchKernelGGL((rs104_ragged_kernel<false, false>), grid, dim3(kThreads), 0, stream, r);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 template <bool DEC, bool XORONLY, int TB>

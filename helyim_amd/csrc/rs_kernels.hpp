@@ -75,6 +75,7 @@ struct RaggedArgs {
     uint32_t* bad_count;
     uint32_t compact;            // decode: inputs = slots 0..9 at off (the first 10 present
                                  // shards), outputs = slots 0..e-1 at out_off (erased shards)
+    uint32_t block_base;         // launcher-internal: first map entry of this launch
 };
 
 hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream);

@@ -567,3 +567,36 @@ def test_batch_over_launch_limit_is_split(gpu):
     assert int(bad.item()) == 0
     assert torch.equal(t[idx], want)
     assert int(t[:, 13].sum(dtype=torch.int64).item()) > 0  # last range rebuilt too
+
+
+def test_ragged_over_launch_limit_is_split(gpu):
+    """2^24 + 5 ragged stripes of 16 B (one workgroup each): the ragged
+    launchers split the workgroup map into launches of kMaxLaunchBlocks.
+    Descriptors go straight to the C ABI (numpy), not the per-row helper."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = (1 << 24) + 5, 16
+    t = torch.empty((S, 14, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t, 10 * L, 0x5EED2000)
+    dt = np.dtype([("offset", "<u8"), ("shard_stride", "<u8"), ("shard_len", "<u4"), ("present_mask", "<u4")])
+    d = np.zeros(S, dtype=dt)
+    d["offset"] = np.arange(S, dtype=np.uint64) * (14 * L)
+    d["shard_stride"] = L
+    d["shard_len"] = L
+    st = torch.cuda.current_stream().cuda_stream
+    assert H.lib.hec_gpu_encode_ragged(rs.handle, t.data_ptr(), d.ctypes.data, S, st) == 0
+    torch.cuda.synchronize()
+    idx = torch.tensor([0, (1 << 23) - 1, 1 << 23, (1 << 24) - 1, 1 << 24, S - 1], device="cuda")
+    host = t[idx].cpu().numpy()
+    assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
+    want = t[idx].clone()
+    d["present_mask"] = 0x3FFF & ~0b01000000010011  # shards 0, 1, 4, 12 erased
+    for i in (0, 1, 4, 12):
+        t[:, i] = 0
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    assert H.lib.hec_gpu_reconstruct_ragged(rs.handle, t.data_ptr(), d.ctypes.data, S, bad.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0
+    assert torch.equal(t[idx], want)

@@ -117,26 +117,45 @@ def host_reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks
     return int(bad.value)
 
 
-def _desc_array(descs, base: torch.Tensor, shards: int):
-    """descs: iterable of (offset, shard_stride, shard_len, present_mask).
-    Every stripe's bytes [offset, offset + (shards-1)*stride + len) must lie
-    inside ``base`` (checked here: the C ABI only sees a pointer)."""
+DESC_DTYPE = None
+
+
+def desc_dtype():
+    """numpy dtype of include/hec.h ``hec_stripe_desc`` (24 bytes)."""
     import numpy as np
-    dt = np.dtype([("offset", "<u8"), ("shard_stride", "<u8"), ("shard_len", "<u4"), ("present_mask", "<u4")])
-    d = np.array([tuple(int(x) for x in r) for r in descs], dtype=dt)
+    global DESC_DTYPE
+    if DESC_DTYPE is None:
+        DESC_DTYPE = np.dtype([("offset", "<u8"), ("shard_stride", "<u8"), ("shard_len", "<u4"),
+                               ("present_mask", "<u4")])
+    return DESC_DTYPE
+
+
+def _desc_array(descs, base: torch.Tensor, shards: int):
+    """descs: a ``desc_dtype()`` array, or rows of (offset, shard_stride,
+    shard_len, present_mask). Every stripe's bytes [offset, offset +
+    (shards-1)*stride + len) must lie inside ``base`` (checked here: the C ABI
+    only sees a pointer)."""
+    import numpy as np
+    dt = desc_dtype()
+    if isinstance(descs, np.ndarray) and descs.dtype == dt:
+        d = np.ascontiguousarray(descs)
+    else:
+        d = np.array([tuple(int(x) for x in r) for r in descs], dtype=dt)
     if base.dtype != torch.uint8 or not base.is_cuda or not base.is_contiguous():
         raise TypeError("base must be a contiguous uint8 CUDA tensor")
     _check_device(base)
     if len(d):
-        off = d["offset"].astype(object)
-        end = off + (shards - 1) * d["shard_stride"].astype(object) + d["shard_len"].astype(object)
-        big = [i for i in range(len(d)) if end[i] > base.numel()
-               or (d["shard_len"][i] and d["shard_stride"][i] < d["shard_len"][i])]
-        if big:
-            i = big[0]
-            raise ValueError(f"stripe {i} (offset {int(d['offset'][i])}, stride {int(d['shard_stride'][i])}, "
-                             f"len {int(d['shard_len'][i])}) overlaps itself or runs past base "
-                             f"({base.numel()} bytes)")
+        off, stride, ln = d["offset"], d["shard_stride"], d["shard_len"].astype(np.uint64)
+        limit = np.uint64(base.numel())
+        # no wrap-around: every term is checked against the buffer before summing
+        bad = (off > limit) | (stride > limit) | (ln > limit)
+        end = off + np.uint64(shards - 1) * np.minimum(stride, limit) + ln
+        bad |= end > limit
+        bad |= (ln > 0) & (stride < ln)
+        if bad.any():
+            i = int(np.argmax(bad))
+            raise ValueError(f"stripe {i} (offset {int(off[i])}, stride {int(stride[i])}, len {int(ln[i])}) "
+                             f"overlaps itself or runs past base ({base.numel()} bytes)")
     return d
 
 

@@ -50,14 +50,15 @@ def test_c_client_parity(gpu, tmp_path):
 @pytest.mark.gpu
 def test_c_abi_bench_small(gpu):
     """tools/cabi_bench.cpp (built by `make all`): the bench workload through
-    the C ABI alone, at 64 stripes, must verify its sampled rebuilds."""
+    the C ABI alone, 64 stripes on each of 2 worker threads (each selecting
+    its device with hec_set_device), must verify its sampled rebuilds."""
     import json
     exe = os.path.join(ROOT, "build", "cabi_bench")
     if not os.path.exists(exe):
         pytest.fail("build/cabi_bench not built (run make)")
     env = dict(os.environ)
     env.pop("HEC_LIB_PATH", None)
-    r = subprocess.run([exe, "64", "2", "1"], capture_output=True, text=True, timeout=120, env=env)
+    r = subprocess.run([exe, "64", "2", "1", "2"], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out["verified"] is True and out["stripes"] == 64
+    assert out["verified"] is True and out["stripes_per_worker"] == 64 and out["workers"] == 2

@@ -600,3 +600,36 @@ def test_ragged_over_launch_limit_is_split(gpu):
     torch.cuda.synchronize()
     assert int(bad.item()) == 0
     assert torch.equal(t[idx], want)
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (12, 4), (8, 8), (1, 1)])
+def test_device_batches_generic_geometry(gpu, k, m):
+    """hec_gpu_encode_batch / hec_gpu_reconstruct_batch on geometries other
+    than RS(10,4) (the generic plan kernel; total shards <= 16 for device
+    masks), per-stripe random erasure patterns, against the C oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rng = np.random.default_rng(77 * k + m)
+    n = k + m
+    rs, ors = H.ReedSolomon(k, m), corc.CReedSolomon(k, m)
+    for S, L in ((5, 1), (7, 4099), (3, 65536)):
+        host = np.zeros((S, n, L), np.uint8)
+        host[:, :k] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+        for s in range(S):
+            ors.encode([host[s, i] for i in range(n)])
+        t = torch.zeros((S, n, L), dtype=torch.uint8, device="cuda")
+        t[:, :k] = torch.from_numpy(host[:, :k]).cuda()
+        B.encode_batch(rs, t)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), host), (k, m, S, L)
+        masks = np.full(S, (1 << n) - 1, np.int64)
+        for s in range(S):
+            for i in rng.choice(n, int(rng.integers(0, m + 1)), replace=False):
+                masks[s] &= ~(1 << int(i))
+                t[s, int(i)] = 0x5A
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        B.reconstruct_batch(rs, t, torch.from_numpy(masks.astype(np.int32)).cuda(), bad)
+        torch.cuda.synchronize()
+        assert int(bad.item()) == 0
+        assert np.array_equal(t.cpu().numpy(), host), (k, m, S, L)

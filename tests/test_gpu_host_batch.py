@@ -94,3 +94,33 @@ def test_mixed_workload_lengths(gpu):
         assert torch.equal(t, good)
         ref = corc.encode_stripes(np.ascontiguousarray(good.numpy()[:, :10]))
         assert np.array_equal(good.numpy()[:, 10:], ref)
+
+
+@pytest.mark.parametrize("k,m,pin", [(3, 2, True), (6, 3, False), (12, 4, True), (8, 8, False)])
+def test_host_batches_generic_geometry(gpu, k, m, pin):
+    """Host batches on geometries other than RS(10,4) (pinned: zero copy or
+    pipeline; pageable: pooled staging), seeded per-stripe erasures, against
+    the C oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rng = np.random.default_rng(31 * k + m)
+    n, S, L = k + m, 6, 4096 + 7
+    rs, ors = H.ReedSolomon(k, m), corc.CReedSolomon(k, m)
+    t = torch.zeros((S, n, L), dtype=torch.uint8)
+    if pin:
+        t = t.pin_memory()
+    a = t.numpy()
+    a[:, :k] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    want = a.copy()
+    for s in range(S):
+        ors.encode([want[s, i] for i in range(n)])
+    B.host_encode_batch(rs, t)
+    assert np.array_equal(a, want)
+    masks = np.full(S, (1 << n) - 1, np.uint32)
+    for s in range(S):
+        for i in rng.choice(n, int(rng.integers(0, m + 1)), replace=False):
+            masks[s] &= ~np.uint32(1 << int(i))
+            a[s, int(i)] = 0xC3
+    assert B.host_reconstruct_batch(rs, t, masks) == 0
+    assert np.array_equal(a, want)

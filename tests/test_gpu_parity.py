@@ -633,3 +633,59 @@ def test_device_batches_generic_geometry(gpu, k, m):
         torch.cuda.synchronize()
         assert int(bad.item()) == 0
         assert np.array_equal(t.cpu().numpy(), host), (k, m, S, L)
+
+
+def test_randomised_device_batches_vs_oracle(gpu):
+    """Seeded sweep over the device batch API: shard lengths (tiny, odd,
+    16-byte and 8 KiB multiples), shard pitches (tight, padded, unaligned),
+    in-place and separate parity buffers, per-stripe erasure patterns, and
+    every kernel-selection knob (encode kernel, workgroup size, XCD remap,
+    vectors per lane), all against the C oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rng = np.random.default_rng(20261016)
+    rs = H.ReedSolomon(10, 4)
+    lib = H.lib
+    lens = [1, 15, 16, 17, 100, 4080, 4096, 4112, 8192, 12288, 16384, 24576, 65536, 65536 + 48, 100003]
+    try:
+        for case in range(120):
+            L = int(rng.choice(lens))
+            S = int(rng.integers(1, 9))
+            pad = int(rng.choice([0, 16, 48, 4096, 3]))
+            sep = bool(rng.integers(0, 2))
+            assert lib.hec_set_encode_kernel(int(rng.integers(0, 2))) == 0
+            assert lib.hec_set_workgroup_size(int(rng.choice([128, 256, 512]))) == 0
+            B.set_launch_config(vec_per_thread=int(rng.choice([1, 2])), xcd_remap=int(rng.integers(0, 2)))
+            P = L + pad
+            raw = torch.zeros(S * 14 * P + 16, dtype=torch.uint8, device="cuda")
+            t = raw[:S * 14 * P].view(S, 14, P)[:, :, :L]
+            host = np.zeros((S, 14, L), np.uint8)
+            host[:, :10] = rng.integers(0, 256, (S, 10, L), dtype=np.uint8)
+            host[:, 10:] = corc.encode_stripes(np.ascontiguousarray(host[:, :10]))
+            t[:, :10] = torch.from_numpy(host[:, :10]).cuda()
+            if sep:
+                par_raw = torch.zeros(S * 4 * P + 16, dtype=torch.uint8, device="cuda")
+                par = par_raw[:S * 4 * P].view(S, 4, P)[:, :, :L]
+                B.encode_batch_sep(rs, t[:, :10], par)
+                torch.cuda.synchronize()
+                assert np.array_equal(par.cpu().numpy(), host[:, 10:]), (case, L, S, pad)
+                t[:, 10:] = par
+            else:
+                B.encode_batch(rs, t)
+                torch.cuda.synchronize()
+                assert np.array_equal(t.cpu().numpy(), host), (case, L, S, pad)
+            masks = np.full(S, 0x3FFF, np.int64)
+            for s in range(S):
+                for i in rng.choice(14, int(rng.integers(0, 5)), replace=False):
+                    masks[s] &= ~(1 << int(i))
+                    t[s, int(i)] = 0xEE
+            bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+            B.reconstruct_batch(rs, t, torch.from_numpy(masks.astype(np.int32)).cuda(), bad)
+            torch.cuda.synchronize()
+            assert int(bad.item()) == 0
+            assert np.array_equal(t.cpu().numpy(), host), (case, L, S, pad, "decode")
+    finally:
+        lib.hec_set_encode_kernel(1)
+        lib.hec_set_workgroup_size(256)
+        B.set_launch_config()

@@ -689,3 +689,58 @@ def test_randomised_device_batches_vs_oracle(gpu):
         lib.hec_set_encode_kernel(1)
         lib.hec_set_workgroup_size(256)
         B.set_launch_config()
+
+
+def test_randomised_ragged_batches_vs_oracle(gpu):
+    """Seeded sweep over ragged device batches: per-stripe lengths (all 8 KiB
+    multiples -> bit-sliced ragged encode, or mixed -> table kernel), padded
+    strides and gaps, 0..5 erasures per stripe (5 = skipped and counted)."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rng = np.random.default_rng(1016)
+    rs = H.ReedSolomon(10, 4)
+    for case in range(40):
+        n = int(rng.integers(1, 25))
+        if case % 2:
+            lens = [8192 * int(rng.integers(1, 9)) for _ in range(n)]
+        else:
+            lens = [int(rng.choice([1, 17, 4096, 5000, 8192, 65536 + 16, 70001])) for _ in range(n)]
+        descs, off = [], 0
+        for L in lens:
+            stride = (L + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+            off += 16 * int(rng.integers(0, 4))
+            descs.append([off, stride, L, 0x3FFF])
+            off += 14 * stride
+        host = np.zeros(off, np.uint8)
+        want = []
+        for o, st, L, _ in descs:
+            data = rng.integers(0, 256, (10, L), dtype=np.uint8)
+            par = corc.encode_stripes(data[None].copy())[0]
+            for i in range(10):
+                host[o + i * st: o + i * st + L] = data[i]
+            want.append(np.concatenate([data, par]))
+        buf = torch.from_numpy(host).cuda()
+        B.encode_ragged(rs, buf, descs)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        for j, (o, st, L, _) in enumerate(descs):
+            for i in range(14):
+                assert np.array_equal(got[o + i * st: o + i * st + L], want[j][i]), (case, j, i)
+        n_bad = 0
+        for d in descs:
+            e = int(rng.integers(0, 6))
+            n_bad += e == 5
+            for i in rng.choice(14, e, replace=False):
+                d[3] &= ~(1 << int(i))
+                buf[d[0] + int(i) * d[1]: d[0] + int(i) * d[1] + d[2]] = 0x77
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        B.reconstruct_ragged(rs, buf, descs, bad)
+        torch.cuda.synchronize()
+        assert int(bad.item()) == n_bad, case
+        got = buf.cpu().numpy()
+        for j, (o, st, L, m) in enumerate(descs):
+            if bin(m).count("1") < 10:
+                continue
+            for i in range(14):
+                assert np.array_equal(got[o + i * st: o + i * st + L], want[j][i]), (case, j, i, "decode")

@@ -117,9 +117,22 @@ void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>&
         for (size_t i = 0; i < n; ++i) fn(i);
 }
 
-LaunchConfig& launch_config() {
-    static LaunchConfig cfg;
-    return cfg;
+// Process-wide launch knobs (measurement switches, speed only): set under a
+// mutex, read as a snapshot per launch, so concurrent callers never see a
+// half-updated configuration.
+namespace {
+std::mutex g_cfg_mu;
+LaunchConfig g_cfg;
+}  // namespace
+
+LaunchConfig launch_config() {
+    std::lock_guard<std::mutex> lk(g_cfg_mu);
+    return g_cfg;
+}
+
+static void update_launch_config(const std::function<void(LaunchConfig&)>& f) {
+    std::lock_guard<std::mutex> lk(g_cfg_mu);
+    f(g_cfg);
 }
 
 int current_device(int* dev) {
@@ -374,8 +387,8 @@ int Scratch::reserve_host(size_t bytes) {
     return HEC_OK;
 }
 
-bool& zero_copy_enabled() {
-    static bool on = true;
+std::atomic<bool>& zero_copy_enabled() {
+    static std::atomic<bool> on{true};
     return on;
 }
 
@@ -388,8 +401,8 @@ uint8_t* pinned_device_ptr(void* host) {
     return static_cast<uint8_t*>(d);
 }
 
-uint64_t& host_staging_max() {
-    static uint64_t v = uint64_t(16) << 20;  // measured crossover
+std::atomic<uint64_t>& host_staging_max() {
+    static std::atomic<uint64_t> v{uint64_t(16) << 20};  // measured crossover
     return v;
 }
 
@@ -594,35 +607,37 @@ int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, in
     if (vec_per_thread != 1 && vec_per_thread != 2 && vec_per_thread != 4)
         return fail(HEC_ERR_INVALID_ARGUMENT, "vec_per_thread must be 1, 2 or 4");
     if (blocks_per_cu < 0 || blocks_per_cu > 8) return fail(HEC_ERR_INVALID_ARGUMENT, "blocks_per_cu in 0..8");
-    launch_config().vec_per_thread = vec_per_thread;
-    launch_config().max_blocks = max_blocks < 0 ? 0 : max_blocks;
     if (xcd_remap < 0) return fail(HEC_ERR_INVALID_ARGUMENT, "xcd_remap >= 0");
-    launch_config().xcd_remap = xcd_remap;
-    launch_config().blocks_per_cu = blocks_per_cu;
+    update_launch_config([&](LaunchConfig& c) {
+        c.vec_per_thread = vec_per_thread;
+        c.max_blocks = max_blocks < 0 ? 0 : max_blocks;
+        c.xcd_remap = xcd_remap;
+        c.blocks_per_cu = blocks_per_cu;
+    });
     return HEC_OK;
 }
 
 int hec_set_xcd_parts(int parts) {
     if (parts < 1 || parts > 1024) return fail(HEC_ERR_INVALID_ARGUMENT, "parts in 1..1024");
-    launch_config().xcd_parts = parts;
+    update_launch_config([&](LaunchConfig& c) { c.xcd_parts = parts; });
     return HEC_OK;
 }
 
 int hec_set_chunk_rotation(int on) {
-    launch_config().chunk_rot = on ? 1 : 0;
+    update_launch_config([&](LaunchConfig& c) { c.chunk_rot = on ? 1 : 0; });
     return HEC_OK;
 }
 
 int hec_set_workgroup_size(int threads) {
     if (threads != 128 && threads != 256 && threads != 512 && threads != 1024)
         return fail(HEC_ERR_INVALID_ARGUMENT, "workgroup size must be 128, 256, 512 or 1024");
-    launch_config().wg_threads = threads;
+    update_launch_config([&](LaunchConfig& c) { c.wg_threads = threads; });
     return HEC_OK;
 }
 
 int hec_set_encode_kernel(int kind) {
     if (kind != 0 && kind != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0 or 1");
-    launch_config().bitslice = kind;
+    update_launch_config([&](LaunchConfig& c) { c.bitslice = kind; });
     return HEC_OK;
 }
 
@@ -633,7 +648,7 @@ int hec_set_host_staging(uint64_t max_bytes) {
 
 int hec_set_kernel_mode(int mode) {
     if (mode != 0 && mode != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "mode must be 0 or 1");
-    launch_config().mode = mode;
+    update_launch_config([&](LaunchConfig& c) { c.mode = mode; });
     return HEC_OK;
 }
 

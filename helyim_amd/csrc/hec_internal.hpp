@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <mutex>
@@ -92,7 +93,7 @@ struct GeomDevice {
 int geom_device(const hec_rs* rs, GeomDevice** out);
 int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s);
 
-LaunchConfig& launch_config();
+LaunchConfig launch_config();  // snapshot of the process-wide knobs
 int current_device(int* dev);
 
 // Per-device scratch for host-memory entry points (serialised by mu).
@@ -111,13 +112,13 @@ int device_scratch(Scratch** out);
 
 // Zero-copy switch (hec_set_host_zero_copy): pinned host memory the GPU can
 // address is coded by the kernels in place over PCIe instead of being copied.
-bool& zero_copy_enabled();
+std::atomic<bool>& zero_copy_enabled();
 // Device address of a hipHostMalloc'd pinned buffer (nullptr if unavailable).
 uint8_t* pinned_device_ptr(void* host);
 
 // Host calls whose k * shard_len input is at most this many bytes go through
 // pinned staging (one H2D, one D2H) instead of one pageable copy per shard.
-uint64_t& host_staging_max();
+std::atomic<uint64_t>& host_staging_max();
 
 // Batched RS(10,4) reconstruct of independent stripes through pinned compact
 // staging and one rs104_ragged_kernel launch (intervals.cpp). Job j has shard

@@ -251,7 +251,8 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     std::vector<uint32_t> block_item;
     items.reserve(n);
     // encode of lengths that are all multiples of 8 KiB: the bit-sliced kernel
-    bool bitslice = !decode && launch_config().bitslice != 0 && launch_config().mode == 0;
+    const LaunchConfig cfg = launch_config();
+    bool bitslice = !decode && cfg.bitslice != 0 && cfg.mode == 0;
     for (uint32_t j = 0; j < n && bitslice; ++j) bitslice = descs[j].shard_len % kBsChunk == 0;
     const uint32_t chunk_bytes = bitslice ? kBsChunk : 4096;
     for (uint32_t j = 0; j < n; ++j) {

@@ -141,6 +141,11 @@ def main():
     th = [threading.Thread(target=worker, args=(i,)) for i in range(args.threads)]
     for t in th:
         t.start()
+    while any(t.is_alive() for t in th):  # progress line every 30 s (long runs must not look hung)
+        next(t for t in th if t.is_alive()).join(timeout=30.0)
+        with lock:
+            print(json.dumps({"progress_s": round(time.monotonic() - t0, 1), "ops": dict(counts),
+                              "failures": len(failures)}), file=sys.stderr, flush=True)
     for t in th:
         t.join()
     out = {"tool": "stress", "threads": args.threads, "seconds": round(time.monotonic() - t0, 1),

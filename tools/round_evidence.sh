@@ -8,3 +8,5 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 120 ./build/cabi_bench > $OUT/cabi_bench.json 2>&1
 bash tools/profile.sh $TAG
+python tools/pmc_summary.py $OUT $OUT/pmc_traffic.json > /dev/null
+python tools/sq_summary.py $OUT/pmc_sq/run_counter_collection.csv $OUT/pmc_sq_wave_states.json > /dev/null

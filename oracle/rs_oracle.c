@@ -6,7 +6,8 @@
  * lives in the un-vendored crate reed-solomon-erasure 6.0.0 (git
  * helyim/reed-solomon-erasure, branch main, feature simd-accel;
  * /root/reference/Cargo.toml:72). Used by tests/ (bit-exact checker on the GPU
- * box) and by bench.py's cpu_baseline leg (the timed CPU path, kind "port").
+ * box), by bench.py's cpu_baseline leg (the timed CPU path, kind "port") and
+ * by the measurement tools under tools/ (checker and CPU baseline).
  * Never linked into or called by the product library helyim_amd/libhec.so.
  *
  * Two encode kernels, selected by the caller:

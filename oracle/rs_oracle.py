@@ -2,8 +2,10 @@
 
 This module is the numpy restatement of the algorithm behind helyim-ec's
 erasure coding. It exists to CHECK the HIP product path (helyim_amd/libhec.so);
-it is never the thing measured or shipped. Only tests/, __graft_entry__.smoke()
-and bench.py's cpu_baseline leg may import it.
+it is never the thing measured or shipped. Only tests/, __graft_entry__.smoke(),
+bench.py's cpu_baseline leg and the measurement tools under tools/ (as the
+checker of GPU outputs and as the timed CPU baseline beside them) import it;
+the product package helyim_amd/ never does.
 
 Provenance of the algorithm (the reference cannot be built here: Rust toolchain
 absent, and the arithmetic lives in the un-vendored git dependency

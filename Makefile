@@ -29,7 +29,7 @@ build/cabi_bench: tools/cabi_bench.cpp include/hec.h helyim_amd/libhec.so
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lhelyim_amd -lhec -Wl,-rpath,'$$ORIGIN/../helyim_amd'
 
 # Measurement variants of the kernel file (cache policy of shard streams).
-VARIANTS := ntl0_nts0 ntl0_nts1 ntl1_nts0
+VARIANTS := ntl0_nts0 ntl0_nts1 ntl1_nts0 null
 variants: $(foreach v,$(VARIANTS),build/variants/libhec_$(v).so)
 build/variants/libhec_%.so: $(SRC) $(HDR)
 	@mkdir -p build/variants/$*
@@ -39,6 +39,7 @@ build/variants/libhec_%.so: $(SRC) $(HDR)
 VFLAGS_ntl0_nts0 := -DHEC_NT_LOAD=0 -DHEC_NT_STORE=0
 VFLAGS_ntl0_nts1 := -DHEC_NT_LOAD=0 -DHEC_NT_STORE=1
 VFLAGS_ntl1_nts0 := -DHEC_NT_LOAD=1 -DHEC_NT_STORE=0
+VFLAGS_null := -DHEC_NULL_VARIANT=1  # identical code: measures the A/B method itself
 
 clean:
 	rm -rf build helyim_amd/libhec.so

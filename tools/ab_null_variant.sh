@@ -2,7 +2,7 @@
 # build linked as a variant (null), in interleaved order. Spread = method noise.
 TAG=${1:-abn}
 mkdir -p gpurun_out/$TAG; : > gpurun_out/$TAG/ab.log
-for v in ship null null ship ship null; do
+for v in ${VARS:-ship null null ship ship null}; do
   if [ $v = ship ]; then L=""; else L=build/variants/libhec_$v.so; fi
   echo "== $v" >> gpurun_out/$TAG/ab.log
   HEC_LIB_PATH=$L timeout -k 10 200 python tools/tune.py --modes 0 --vecs 1 --blocks 0 --remaps 1 --bpcs 0 \

@@ -11,17 +11,26 @@ stripes generated in HBM before the timed region.
 
 value = data-payload GiB/s over all ranks: (encode 10*L + decode 10*L bytes
 per stripe) * stripes * ranks / max-over-ranks step time. Multi-GPU: one
-process per GPU (torchrun), independent stripe batches per rank (seed base
+process per GPU, independent stripe batches per rank (seed base
 0x5EED0000 + rank*2^20), no data-path collective ("scaling": "weak"); the
-only cross-rank traffic is the barrier and the max-reduce of the timings.
+only cross-rank traffic is the barrier and the max-reduce of the timings
+(gloo, host side).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  Without WORLD_SIZE in the environment and N > 1, this process is only a
+  launcher: it makes no GPU call, starts N ranks with torch.distributed.run
+  (127.0.0.1 rendezvous) and exits with their status. Under an external
+  launcher WORLD_SIZE must equal N. --dry-run runs the launcher and the
+  control plane (seeds, barrier, max-over-ranks timing, aggregation) with a
+  GPU-free stand-in step (tests/test_bench_launcher.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -69,10 +78,121 @@ def reduce_max(x: float, world: int) -> float:
     return float(v.item())
 
 
+def gather(obj, world: int) -> list:
+    """Every rank's `obj` (control plane only: gloo all_gather_object)."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def job_throughput(payload_bytes_per_rank_step: float, steps: int, world: int, t_job: float) -> float:
     """Whole-job GiB/s: every rank processes the same payload per step; the
     job's time is the max over ranks."""
     return payload_bytes_per_rank_step * steps * world / t_job / 2**30
+
+
+def aggregate_host_path(per_rank: list) -> dict:
+    """Whole-node host-path rate from per-rank legs that ran concurrently
+    (started after one barrier): bytes of all ranks / the slowest rank's time,
+    per direction. per_rank entries: {"data_bytes", "encode_s", "decode_s"}."""
+    data = sum(r["data_bytes"] for r in per_rank)
+    te = max(r["encode_s"] for r in per_rank)
+    td = max(r["decode_s"] for r in per_rank)
+    return {"ranks": len(per_rank),
+            "encode_data_GiB_s": round(data / te / 2**30, 2),
+            "decode_data_GiB_s": round(data / td / 2**30, 2),
+            "per_rank_encode_data_GiB_s": [round(r["data_bytes"] / r["encode_s"] / 2**30, 2) for r in per_rank],
+            "per_rank_decode_data_GiB_s": [round(r["data_bytes"] / r["decode_s"] / 2**30, 2) for r in per_rank]}
+
+
+# ---------------------------------------------------------------------------
+# launcher (no GPU call in this process)
+# ---------------------------------------------------------------------------
+def visible_gpu_count() -> int:
+    """GPUs a child process could open, counted without initialising HIP:
+    the first *_VISIBLE_DEVICES list that is set, else the KFD topology nodes
+    that have SIMDs (GPU agents)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    for line in f:
+                        k, _, v = line.partition(" ")
+                        if k == "simd_count" and int(v) > 0:
+                            n += 1
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    return n
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args, argv: list) -> int:
+    """Start args.gpus ranks of this script (torch.distributed.run as a child
+    process, one rank per GPU) and return their exit status."""
+    n = args.gpus
+    if not args.dry_run:
+        have = visible_gpu_count()
+        if n > have and not args.allow_shared_gpu:
+            log(f"bench.py: --gpus {n} but {have} GPU(s) visible; refusing "
+                f"(--allow-shared-gpu rehearses more ranks than GPUs)")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def physical_cores() -> dict:
+    """lscpu-equivalent counts from sysfs: physical cores (distinct
+    (package, core) pairs), logical CPUs, and what this process may use
+    (affinity mask, cgroup v2 cpu.max quota)."""
+    base = "/sys/devices/system/cpu"
+    cores, logical = set(), 0
+    try:
+        for d in os.listdir(base):
+            if not (d.startswith("cpu") and d[3:].isdigit()):
+                continue
+            try:
+                with open(f"{base}/{d}/topology/physical_package_id") as f:
+                    pkg = f.read().strip()
+                with open(f"{base}/{d}/topology/core_id") as f:
+                    core = f.read().strip()
+            except OSError:
+                continue
+            logical += 1
+            cores.add((pkg, core))
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            if q != "max":
+                quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return {"physical_cores": len(cores) or (os.cpu_count() or 1), "logical_cpus": logical or os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(seconds: float = 10.0) -> dict:
@@ -157,12 +277,18 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+TRAFFIC_FILE = "profiles/pmc_traffic.json"
+
+
 def load_traffic() -> dict:
-    """HBM traffic per launch from the committed rocprofv3 PMC summary, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """HBM traffic per launch from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py), if any; "_file" names it for the bench line."""
+    p = os.path.join(ROOT, TRAFFIC_FILE)
     if os.path.exists(p):
         with open(p) as f:
-            return json.load(f)
+            d = json.load(f)
+        d["_file"] = TRAFFIC_FILE
+        return d
     return {}
 
 
@@ -171,10 +297,12 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) ->
     stripes -> H2D -> kernel -> D2H, pipelined over 3 streams. Encode moves
     10 L H2D + 4 L D2H per stripe; a 4-erasure decode 10 L H2D + 4 L D2H."""
     import torch
+    import helyim_amd as H
     import helyim_amd.batch as B
     dev = torch.empty((S, N_TOTAL, L), dtype=torch.uint8, device="cuda")
     B.fill_splitmix(dev, K_DATA * L, rank_seed_base(rank))
-    host = torch.empty((S, N_TOTAL, L), dtype=torch.uint8).pin_memory()
+    buf = H.HostBuffer(S * N_TOTAL * L)  # pinned, on this GPU's NUMA node
+    host = buf.tensor((S, N_TOTAL, L))
     host.copy_(dev)
     del dev
     masks = erasure_masks(S, rank)
@@ -189,7 +317,12 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) ->
         B.host_reconstruct_batch(rs, host, masks)
     td = (time.perf_counter() - t0) / reps
     data = S * K_DATA * L
-    return {"stripes": S, "shard_len": L, "host_memory": "pinned (torch pin_memory)",
+    node = buf.numa_node()
+    del host
+    buf.close()
+    return {"stripes": S, "shard_len": L, "host_memory": "pinned (hec_host_alloc: this GPU's NUMA node)",
+            "host_numa_node": node,
+            "raw": {"data_bytes": data, "encode_s": te, "decode_s": td},
             "encode_data_GiB_s": round(data / te / 2**30, 2),
             "decode_data_GiB_s": round(data / td / 2**30, 2),
             "encode_pcie_GB_s": round(S * N_TOTAL * L / te / 1e9, 2),
@@ -202,6 +335,7 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
     one ragged encode launch + one ragged reconstruct launch. End to end: the
     pinned-host pipeline (hec_host_*_batch), one call per length group."""
     import torch
+    import helyim_amd as H
     import helyim_amd.batch as B
     rng = np.random.default_rng(0x5E + rank)
     lens = [(64 << 10) << i for i in range(7)]
@@ -235,12 +369,14 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
     e1.record(s_)
     torch.cuda.synchronize()
     t_dev = e0.elapsed_time(e1) * 1e-3 / reps
-    groups = []
+    groups, bufs = [], []
     for L in lens:
         idx = [s for s in range(n_stripes) if Ls[s] == L]
         if not idx:
             continue
-        h = torch.empty((len(idx), N_TOTAL, L), dtype=torch.uint8).pin_memory()
+        hb = H.HostBuffer(len(idx) * N_TOTAL * L)  # pinned, on this GPU's NUMA node
+        bufs.append(hb)
+        h = hb.tensor((len(idx), N_TOTAL, L))
         for j, s in enumerate(idx):
             o = descs[s][0]
             h[j].view(-1).copy_(dev[o:o + N_TOTAL * L])
@@ -253,15 +389,35 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
         B.host_encode_batch(rs, h)
         B.host_reconstruct_batch(rs, h, m)
     t_e2e = time.perf_counter() - t0
+    groups.clear()
+    for hb in bufs:
+        hb.close()
     return {"stripes": n_stripes, "shard_lens": "64 KiB..4 MiB log-uniform", "erasures": "0..4 uniform",
             "payload_GiB": round((data + dec_data) / 2**30, 3),
             "payload": "encode 10 L per stripe + decode 10 L per stripe with >= 1 erasure",
             "device_resident_data_GiB_s": round((data + dec_data) / t_dev / 2**30, 2),
             "device_resident": "one ragged encode + one ragged reconstruct launch over all stripes",
-            "end_to_end_data_GiB_s": round((data + dec_data) / t_e2e / 2**30, 2)}
+            "end_to_end_data_GiB_s": round((data + dec_data) / t_e2e / 2**30, 2),
+            "raw": {"payload_bytes": data + dec_data, "e2e_s": t_e2e, "device_s": t_dev}}
 
 
-def main():
+def init_control_plane() -> None:
+    """gloo process group for the barrier / max-reduce / gather of host
+    scalars. gloo prints its connection report on stdout, which carries only
+    the bench line: fd 1 points at stderr while it connects."""
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", init_method="env://")
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -271,22 +427,94 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the end-to-end and mixed-workload sections")
-    args = ap.parse_args()
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="rehearsal: allow more ranks than visible GPUs (ranks share devices round-robin)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="GPU-free control-plane rehearsal: launcher, seeds, barrier, max-over-ranks timing")
+    ap.add_argument("--dry-step-ms", type=float, default=5.0,
+                    help="dry run: rank r's stand-in step sleeps (r + 1) x this")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus < 1:
+        log("bench.py: --gpus must be >= 1")
+        return 2
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args, argv)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing (one rank per GPU)")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        init_control_plane()
+    try:
+        if args.dry_run:
+            return dry_run(args, world, rank, local_rank)
+        return run_rank(args, world, rank, local_rank)
+    finally:
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+            dist.destroy_process_group()
 
+
+def dry_run(args, world: int, rank: int, local_rank: int) -> int:
+    """The control plane of run_rank with a GPU-free stand-in step (rank r
+    sleeps (r + 1) x dry_step_ms): same barrier, max-over-ranks job time and
+    whole-job throughput formula, one JSON line from rank 0."""
+    S, L = args.stripes, args.shard_len
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    step = args.dry_step_ms * (rank + 1) / 1e3
+    for _ in range(args.warmup):
+        time.sleep(step)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(step)
+    barrier()
+    wall = time.perf_counter() - t0
+    per_rank = gather({"rank": rank, "local_rank": local_rank, "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+                       "seed_base": rank_seed_base(rank), "wall_s": wall, "pid": os.getpid(),
+                       "masks_head": erasure_masks(4, rank).tolist()}, world)
+    t_job = reduce_max(wall, world)
+    if rank == 0:
+        payload = 2 * S * K_DATA * L
+        print(json.dumps({"metric": "dry run (no GPU): launcher and control plane only", "dry_run": True,
+                          "value": round(job_throughput(payload, args.steps, world, t_job), 4), "unit": "GiB/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(t_job / args.steps * 1e3, 4), "scaling": "weak",
+                          "rank_seed_bases": [r["seed_base"] for r in per_rank], "ranks": per_rank}), flush=True)
+    return 0
+
+
+def run_rank(args, world: int, rank: int, local_rank: int) -> int:
     import torch
     import torch.distributed as dist
-    if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
-    # one process per GPU; more ranks than visible GPUs (a rehearsal on a
-    # one-GPU box) share devices round-robin
-    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    # one process per GPU; more ranks than visible GPUs (an --allow-shared-gpu
+    # rehearsal) share devices round-robin
+    ndev = max(1, torch.cuda.device_count())
+    if world > ndev and not args.allow_shared_gpu:
+        log(f"bench.py: {world} ranks but {ndev} GPU(s) visible; refusing (--allow-shared-gpu to rehearse)")
+        return 2
+    device = local_rank % ndev
+    torch.cuda.set_device(device)
 
     import helyim_amd as H
     import helyim_amd.batch as B
+
+    allowed = os.sched_getaffinity(0)
+    numa = H.bind_host_to_device(device)  # this rank's host threads next to its GPU's pinned buffers
 
     S, L = args.stripes, args.shard_len
     rs = H.ReedSolomon(K_DATA, M_PARITY)
@@ -321,7 +549,6 @@ def main():
     t_job = reduce_max(wall, world)
 
     # correctness of what was timed: zero the erased shards, rebuild, compare
-    full = (1 << N_TOTAL) - 1
     chk_ok = True
     sample = slice(0, min(S, 256))
     ref_par = t[sample, K_DATA:].clone()
@@ -343,8 +570,11 @@ def main():
     del t
     # every rank's verification counts: the job is verified only if all are
     chk_ok = reduce_max(0.0 if chk_ok else 1.0, world) == 0.0
-    enc_ms = reduce_max(enc_ms, world)
-    dec_ms = reduce_max(dec_ms, world)
+    per_rank = gather({"rank": rank, "device": device, "seed_base": rank_seed_base(rank), "numa": numa,
+                       "wall_s": round(wall, 6), "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4)},
+                      world)
+    enc_ms = max(r["encode_ms"] for r in per_rank)
+    dec_ms = max(r["decode_ms"] for r in per_rank)
 
     enc_bytes = S * N_TOTAL * L                      # read 10 L + write 4 L per stripe
     dec_bytes = S * (K_DATA + 4) * L                 # read 10 survivors + write 4 erased
@@ -352,7 +582,27 @@ def main():
     value = job_throughput(payload, args.steps, world, t_job)
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
-    traffic = load_traffic().get("encode_hbm_bytes_per_launch")
+    prof = load_traffic()
+
+    extras = {}
+    if not args.no_extras:
+        # host-path legs on every rank at once (after one barrier), so at N > 1
+        # the aggregate shows the shared host-memory / PCIe limit
+        barrier()
+        e2e = e2e_section(rs, rank)
+        barrier()
+        mixed = mixed_section(rs, rank)
+        e2e_all = gather(e2e, world)
+        mixed_all = gather(mixed, world)
+        extras["end_to_end"] = e2e_all[0] if world == 1 else {
+            "aggregate": aggregate_host_path([r["raw"] for r in e2e_all]), "per_rank": e2e_all}
+        if world == 1:
+            extras["mixed"] = mixed_all[0]
+        else:
+            extras["mixed"] = {"per_rank": mixed_all,
+                               "aggregate_end_to_end_data_GiB_s": round(
+                                   sum(m["raw"]["payload_bytes"] for m in mixed_all)
+                                   / max(m["raw"]["e2e_s"] for m in mixed_all) / 2**30, 2)}
 
     if rank == 0:
         out = {
@@ -374,29 +624,33 @@ def main():
                        "parallelism": f"independent stripe batches x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(enc_gbps, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
+                         # PMC counters cannot run inside this process: the HBM bytes per
+                         # launch come from the committed rocprofv3 passes named here
+                         "traffic": prof.get("encode_hbm_bytes_per_launch"),
+                         "traffic_source": prof.get("_file") and f"{prof['_file']} (rocprofv3 FETCH_SIZE/WRITE_SIZE "
+                                                                 f"passes of run {prof.get('source')}; not this run)",
                          "kernel": H.lib.hec_encode_kernel_name(L).decode(),
                          "algorithmic_bytes_per_launch": enc_bytes},
             "encode": {"ms_per_launch": round(enc_ms, 4), "GB_s_hbm": round(enc_gbps, 1),
                        "data_GiB_s": round(S * K_DATA * L / (enc_ms * 1e-3) / 2**30, 1)},
             "decode": {"ms_per_launch": round(dec_ms, 4), "GB_s_hbm": round(dec_gbps, 1),
                        "data_GiB_s": round(S * K_DATA * L / (dec_ms * 1e-3) / 2**30, 1),
-                       "frac": round(dec_gbps / HBM_PEAK_GBPS, 4)},
+                       "frac": round(dec_gbps / HBM_PEAK_GBPS, 4),
+                       "traffic": prof.get("decode_hbm_bytes_per_launch")},
             "verified": chk_ok,
+            "ranks": per_rank,
         }
-        if world == 1 and not args.no_extras:
-            out["end_to_end"] = e2e_section(rs, rank)
-            out["mixed"] = mixed_section(rs, rank)
+        out.update(extras)
         if world == 1 and not args.no_cpu_baseline:
+            os.sched_setaffinity(0, allowed)  # the CPU baseline gets every CPU this process may use
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-            out["cpu_baseline_threads"] = cpu_baseline_threads(args.cpu_seconds / 2)
+            cores = physical_cores()
+            out["cpu_baseline_threads"] = cpu_baseline_threads(args.cpu_seconds / 2, 16)
+            out["cpu_baseline_cores"] = dict(cpu_baseline_threads(args.cpu_seconds / 2, cores["physical_cores"]),
+                                             **cores)
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    if not chk_ok:
-        sys.exit(3)
+    return 0 if chk_ok else 3
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -19,7 +19,7 @@ from .errors import (  # noqa: F401
     NeedleNotFound, ShardNotFound, Underflow, UnexpectedBlockSize, UnexpectedEcShardSize,
 )
 from .rs import ReedSolomon  # noqa: F401
-from .device import device_count, get_device, set_device  # noqa: F401
+from .device import HostBuffer, bind_host_to_device, device_count, get_device, numa_node, set_device  # noqa: F401
 from .ec import (  # noqa: F401
     DATA_SHARDS_COUNT, ERASURE_CODING_LARGE_BLOCK_SIZE, ERASURE_CODING_SMALL_BLOCK_SIZE,
     PARITY_SHARDS_COUNT, TOTAL_SHARDS_COUNT, EcVolume, Interval, find_data_filesize, find_needle_from_ecx, locate_data,

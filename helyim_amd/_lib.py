@@ -96,6 +96,11 @@ SIGNATURES = {
     "hec_device_count": (_I, [ctypes.POINTER(_I)]),
     "hec_set_device": (_I, [_I]),
     "hec_get_device": (_I, [ctypes.POINTER(_I)]),
+    "hec_device_numa_node": (_I, [_I, ctypes.POINTER(_I)]),
+    "hec_bind_thread_to_device": (_I, [_I, ctypes.POINTER(_I)]),
+    "hec_host_alloc": (_I, [_S, ctypes.POINTER(_P)]),
+    "hec_host_free": (_I, [_P]),
+    "hec_host_numa_node": (_I, [_P, ctypes.POINTER(_I)]),
     "hec_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
 }
 

@@ -242,7 +242,7 @@ class FilePipeline {
             if (host_bytes > host_cap_) {
                 if (s.host) HEC_HIP(hipHostFree(s.host));
                 s.host = nullptr;
-                HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.host), host_bytes, hipHostMallocDefault));
+                HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&s.host), host_bytes));
             }
             if (dev_bytes > dev_cap_) {
                 if (s.dev) HEC_HIP(hipFree(s.dev));

@@ -382,7 +382,7 @@ int Scratch::reserve_host(size_t bytes) {
     hbuf = nullptr;
     hcap = 0;
     size_t want = std::max(bytes, size_t(16) << 20);
-    HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&hbuf), want, hipHostMallocDefault));
+    HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&hbuf), want));
     hcap = want;
     return HEC_OK;
 }

@@ -45,6 +45,18 @@ inline int check_strided(const char* what, uint32_t shards, uint64_t stripe_stri
 }
 int hip_fail(hipError_t e, const char* what);
 
+// Propagate a non-zero hec status.
+#define HEC_TRY(call)            \
+    do {                         \
+        int rc_ = (call);        \
+        if (rc_) return rc_;     \
+    } while (0)
+
+// NUMA placement (numa.cpp): node of a GPU's PCI function (-1 unknown), and
+// pinned host memory on the current device's node.
+int device_numa_node(int device, int* node);
+int pinned_alloc(void** p, size_t bytes);
+
 #define HEC_HIP(call)                                          \
     do {                                                       \
         hipError_t e_ = (call);                                \

@@ -37,7 +37,7 @@ struct Pipeline {
             h = nullptr;
         }
         hslot_cap = 0;
-        for (auto& h : hslot) HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault));
+        for (auto& h : hslot) HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&h), bytes));
         hslot_cap = bytes;
         return HEC_OK;
     }
@@ -73,7 +73,7 @@ struct Pipeline {
             mask_cap = 0;
             for (int i = 0; i < kDepth; ++i) {
                 HEC_HIP(hipMalloc(reinterpret_cast<void**>(&mask_dev[i]), n_masks * 4));
-                HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&mask_host[i]), n_masks * 4, hipHostMallocDefault));
+                HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&mask_host[i]), n_masks * 4));
             }
             mask_cap = n_masks;
         }

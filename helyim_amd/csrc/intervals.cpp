@@ -34,7 +34,7 @@ struct RaggedScratch {
             host = dev = nullptr;
             cap = 0;
             const size_t want = std::max(bytes, size_t(64) << 20);
-            HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), want, hipHostMallocDefault));
+            HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&host), want));
             HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dev), want));
             cap = want;
         }
@@ -44,7 +44,7 @@ struct RaggedScratch {
             hmeta = dmeta = nullptr;
             mcap = 0;
             const size_t want = std::max(meta, size_t(1) << 20);
-            HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&hmeta), want, hipHostMallocDefault));
+            HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&hmeta), want));
             HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dmeta), want));
             mcap = want;
         }

@@ -29,3 +29,62 @@ def get_device() -> int:
     d = ctypes.c_int(-1)
     check(lib.hec_get_device(ctypes.byref(d)))
     return d.value
+
+
+def numa_node(device: int) -> int:
+    """NUMA node of the device's PCI function (-1 when the platform does not say)."""
+    n = ctypes.c_int(-1)
+    check(lib.hec_device_numa_node(device, ctypes.byref(n)))
+    return n.value
+
+
+def bind_host_to_device(device: int) -> dict:
+    """Restrict the calling thread -- and the threads it starts later (the
+    library's worker pool, torch's) -- to the device's NUMA node, so the host
+    side of a per-GPU rank runs next to its pinned buffers.
+    Returns what was done: the node, how many CPUs the thread now has."""
+    node = numa_node(device)
+    n = ctypes.c_int(0)
+    check(lib.hec_bind_thread_to_device(device, ctypes.byref(n)))
+    return {"device": device, "gpu_numa_node": node, "bound_cpus": n.value}
+
+
+class HostBuffer:
+    """Pinned host memory on the current device's NUMA node (hec_host_alloc),
+    GPU-addressable, exposed as a numpy array (``.array``) or a torch CPU
+    tensor view (``.tensor(shape)``). Freed by ``close()`` or on collection;
+    views must not outlive it."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        p = ctypes.c_void_p()
+        check(lib.hec_host_alloc(nbytes, ctypes.byref(p)))
+        self._ptr = p.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self._ptr))
+
+    @property
+    def ptr(self) -> int:
+        return self._ptr
+
+    def tensor(self, shape):
+        import torch
+        return torch.from_numpy(self.array).view(*shape)
+
+    def numa_node(self) -> int:
+        """Node holding the buffer's first page."""
+        n = ctypes.c_int(-1)
+        check(lib.hec_host_numa_node(self._ptr, ctypes.byref(n)))
+        return n.value
+
+    def close(self) -> None:
+        if self._ptr:
+            self.array = None
+            check(lib.hec_host_free(self._ptr))
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -80,6 +80,26 @@ int hec_device_count(int* count);  /* HEC_ERR_NO_DEVICE (and 0) without a GPU */
 int hec_set_device(int device);    /* this thread only; HEC_ERR_INVALID_ARGUMENT if out of range */
 int hec_get_device(int* device);
 
+/* ---- NUMA placement of the host side of a GPU (no reference
+ * counterpart: helyim is CPU-only) -------------------------------------------
+ * Every pinned buffer libhec allocates (host-batch and file-layer staging,
+ * small-call staging, degraded-read staging) lives on the NUMA node of the
+ * device it serves. */
+/* sysfs NUMA node of the device's PCI function; -1 when the platform does not
+ * say. */
+int hec_device_numa_node(int device, int* node);
+/* Restrict the calling thread (and threads it creates later) to the CPUs of
+ * the device's NUMA node that it is allowed to run on; *n_cpus (optional) =
+ * how many. No-op (HEC_OK, 0 CPUs) when the node is unknown or none of its
+ * CPUs is in the thread's allowed set. */
+int hec_bind_thread_to_device(int device, int* n_cpus);
+/* Pinned host memory on the current device's NUMA node, addressable by the
+ * GPU (host-batch entry points code it zero-copy). Free with hec_host_free. */
+int hec_host_alloc(size_t bytes, void** out);
+int hec_host_free(void* p);
+/* NUMA node holding the page at p (diagnostic; HEC_ERR_IO if not resident). */
+int hec_host_numa_node(const void* p, int* node);
+
 /* ---- geometry constants (helyim-ec/src/lib.rs:46-50) ---------------------- */
 #define HEC_DATA_SHARDS_COUNT 10u
 #define HEC_PARITY_SHARDS_COUNT 4u

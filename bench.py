@@ -95,17 +95,23 @@ def job_throughput(payload_bytes_per_rank_step: float, steps: int, world: int, t
 
 
 def aggregate_host_path(per_rank: list) -> dict:
-    """Whole-node host-path rate from per-rank legs that ran concurrently
-    (started after one barrier): bytes of all ranks / the slowest rank's time,
-    per direction. per_rank entries: {"data_bytes", "encode_s", "decode_s"}."""
+    """Whole-node host-path rate from per-rank legs run at the same time:
+    bytes of all ranks / the wall-clock window from the first rank's start to
+    the last rank's end, per phase (time.time() stamps, one host clock).
+    per_rank entries: {"data_bytes", "encode": [t0, t1], "decode": [t0, t1]}."""
     data = sum(r["data_bytes"] for r in per_rank)
-    te = max(r["encode_s"] for r in per_rank)
-    td = max(r["decode_s"] for r in per_rank)
+
+    def window(ph):
+        return max(r[ph][1] for r in per_rank) - min(r[ph][0] for r in per_rank)
+
+    def rate(b, t):
+        return round(b / t / 2**30, 2)
+
     return {"ranks": len(per_rank),
-            "encode_data_GiB_s": round(data / te / 2**30, 2),
-            "decode_data_GiB_s": round(data / td / 2**30, 2),
-            "per_rank_encode_data_GiB_s": [round(r["data_bytes"] / r["encode_s"] / 2**30, 2) for r in per_rank],
-            "per_rank_decode_data_GiB_s": [round(r["data_bytes"] / r["decode_s"] / 2**30, 2) for r in per_rank]}
+            "encode_data_GiB_s": rate(data, window("encode")),
+            "decode_data_GiB_s": rate(data, window("decode")),
+            "per_rank_encode_data_GiB_s": [rate(r["data_bytes"], r["encode"][1] - r["encode"][0]) for r in per_rank],
+            "per_rank_decode_data_GiB_s": [rate(r["data_bytes"], r["decode"][1] - r["decode"][0]) for r in per_rank]}
 
 
 # ---------------------------------------------------------------------------
@@ -308,21 +314,21 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) ->
     masks = erasure_masks(S, rank)
     B.host_encode_batch(rs, host)  # warm-up (pipeline buffers, tables)
     B.host_reconstruct_batch(rs, host, masks)
-    t0 = time.perf_counter()
+    enc0 = time.time()
     for _ in range(reps):
         B.host_encode_batch(rs, host)
-    te = (time.perf_counter() - t0) / reps
-    t0 = time.perf_counter()
+    enc1 = dec0 = time.time()
     for _ in range(reps):
         B.host_reconstruct_batch(rs, host, masks)
-    td = (time.perf_counter() - t0) / reps
+    dec1 = time.time()
+    te, td = (enc1 - enc0) / reps, (dec1 - dec0) / reps
     data = S * K_DATA * L
     node = buf.numa_node()
     del host
     buf.close()
     return {"stripes": S, "shard_len": L, "host_memory": "pinned (hec_host_alloc: this GPU's NUMA node)",
             "host_numa_node": node,
-            "raw": {"data_bytes": data, "encode_s": te, "decode_s": td},
+            "raw": {"data_bytes": data * reps, "encode": [enc0, enc1], "decode": [dec0, dec1]},
             "encode_data_GiB_s": round(data / te / 2**30, 2),
             "decode_data_GiB_s": round(data / td / 2**30, 2),
             "encode_pcie_GB_s": round(S * N_TOTAL * L / te / 1e9, 2),
@@ -384,11 +390,12 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
     del dev
     for h, m in groups:
         B.host_encode_batch(rs, h)
-    t0 = time.perf_counter()
+    w0 = time.time()
     for h, m in groups:
         B.host_encode_batch(rs, h)
         B.host_reconstruct_batch(rs, h, m)
-    t_e2e = time.perf_counter() - t0
+    w1 = time.time()
+    t_e2e = w1 - w0
     groups.clear()
     for hb in bufs:
         hb.close()
@@ -398,7 +405,7 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
             "device_resident_data_GiB_s": round((data + dec_data) / t_dev / 2**30, 2),
             "device_resident": "one ragged encode + one ragged reconstruct launch over all stripes",
             "end_to_end_data_GiB_s": round((data + dec_data) / t_e2e / 2**30, 2),
-            "raw": {"payload_bytes": data + dec_data, "e2e_s": t_e2e, "device_s": t_dev}}
+            "raw": {"payload_bytes": data + dec_data, "e2e": [w0, w1], "device_s": t_dev}}
 
 
 def init_control_plane() -> None:
@@ -600,9 +607,11 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
             extras["mixed"] = mixed_all[0]
         else:
             extras["mixed"] = {"per_rank": mixed_all,
+                               # one wall-clock window over every rank's end-to-end part
                                "aggregate_end_to_end_data_GiB_s": round(
                                    sum(m["raw"]["payload_bytes"] for m in mixed_all)
-                                   / max(m["raw"]["e2e_s"] for m in mixed_all) / 2**30, 2)}
+                                   / (max(m["raw"]["e2e"][1] for m in mixed_all)
+                                      - min(m["raw"]["e2e"][0] for m in mixed_all)) / 2**30, 2)}
 
     if rank == 0:
         out = {

@@ -77,9 +77,11 @@ def test_host_path_aggregation():
     sys.path.insert(0, ROOT)
     import bench
     gib = 2**30
-    agg = bench.aggregate_host_path([{"data_bytes": 10 * gib, "encode_s": 0.2, "decode_s": 0.25},
-                                     {"data_bytes": 10 * gib, "encode_s": 0.4, "decode_s": 0.2}])
+    # rank 1 starts its encode 0.1 s late: the node's window is 0.0 .. 0.5 s
+    agg = bench.aggregate_host_path([{"data_bytes": 10 * gib, "encode": [0.0, 0.2], "decode": [0.2, 0.45]},
+                                     {"data_bytes": 10 * gib, "encode": [0.1, 0.5], "decode": [0.5, 0.7]}])
     assert agg["ranks"] == 2
-    assert agg["encode_data_GiB_s"] == 50.0  # 20 GiB / slowest 0.4 s
-    assert agg["decode_data_GiB_s"] == 80.0  # 20 GiB / slowest 0.25 s
+    assert agg["encode_data_GiB_s"] == 40.0  # 20 GiB over 0.5 s
+    assert agg["decode_data_GiB_s"] == 40.0  # 20 GiB over 0.2 .. 0.7 s
     assert agg["per_rank_encode_data_GiB_s"] == [50.0, 25.0]
+    assert agg["per_rank_decode_data_GiB_s"] == [40.0, 50.0]

@@ -262,7 +262,10 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
             d.shard_stride < d.shard_len)
             return fail(HEC_ERR_INVALID_ARGUMENT, "stripe " + std::to_string(j) +
                                                       ": offset/stride must be 16-byte aligned, stride >= len");
-        const uint32_t chunks = (d.shard_len + chunk_bytes - 1) / chunk_bytes;
+        // 64-bit: a shard_len near 2^32 must not wrap to 0 or 1 chunks
+        const uint64_t chunks = (uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes;
+        if (block_item.size() + chunks > UINT32_MAX)
+            return fail(HEC_ERR_INVALID_ARGUMENT, "ragged batch above 2^32 workgroups");
         items.push_back(RaggedItem{d.offset, d.shard_stride, d.shard_len, d.present_mask,
                                    uint32_t(block_item.size()), 0, 0});
         block_item.insert(block_item.end(), chunks, j);

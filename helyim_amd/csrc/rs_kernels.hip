@@ -639,11 +639,26 @@ static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t str
     return hipGetLastError();
 }
 
+// Kernel choice for an aligned RS(10,4) batch, shared by launch_apply and
+// encode_kernel_name so the name reported is the kernel that runs.
+// Fast path: one workgroup per chunk (no grid cap), 1 vector per lane, or 2
+// (pair kernel) when the shard length is a multiple of 8 KiB.
+static bool rs104_fast_ok(uint64_t len, const LaunchConfig& cfg) {
+    const bool pair_ok = cfg.vec_per_thread == 2 && len % (2 * uint64_t(kThreads) * kVecBytes) == 0;
+    return (cfg.vec_per_thread == 1 || pair_ok) && cfg.max_blocks == 0;
+}
+// Bit-sliced encode: GF mode and a shard length that is a multiple of one
+// 2 x workgroup x 16-byte column range.
+static bool rs104_bitslice_ok(uint64_t len, const LaunchConfig& cfg) {
+    return cfg.bitslice && cfg.mode == 0 && len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0;
+}
+
 const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
+    if (!rs104_fast_ok(len, cfg))
+        return cfg.mode == 1 ? "rs_apply_kernel<10, XORONLY=true> (diagnostic)" : "rs_apply_kernel<10> (table lookup)";
     if (cfg.mode == 1) return "rs104_kernel<DEC=false, XORONLY=true> (diagnostic)";
-    if (cfg.bitslice && len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0)
-        return "rs104_bs_encode_kernel (bit-sliced)";
-    if (cfg.vec_per_thread == 2 && len % 8192 == 0) return "rs104_pair_kernel<DEC=false> (table lookup)";
+    if (rs104_bitslice_ok(len, cfg)) return "rs104_bs_encode_kernel (bit-sliced)";
+    if (cfg.vec_per_thread == 2) return "rs104_pair_kernel<DEC=false> (table lookup)";
     return "rs104_kernel<DEC=false> (table lookup)";
 }
 
@@ -668,13 +683,10 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
         }
         return hipSuccess;
     }
-    const bool pair_ok = cfg.vec_per_thread == 2 && a.len % 8192 == 0;
-    if (a.fast104 && aligned && (cfg.vec_per_thread == 1 || pair_ok) && cfg.max_blocks == 0 &&
-        items <= kMaxLaunchBlocks) {
+    if (a.fast104 && aligned && rs104_fast_ok(a.len, cfg) && items <= kMaxLaunchBlocks) {
         if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, cfg, stream)
                                           : launch_rs104<true, false>(a, cfg, stream);
-        if (cfg.bitslice && cfg.mode == 0 && a.len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0)
-            return launch_rs104_bs_cfg(a, cfg, stream);
+        if (rs104_bitslice_ok(a.len, cfg)) return launch_rs104_bs_cfg(a, cfg, stream);
         return cfg.mode == 1 ? launch_rs104<false, true>(a, cfg, stream) : launch_rs104<false, false>(a, cfg, stream);
     }
     if (nin == 10 && aligned && cfg.mode == 1) {

@@ -154,10 +154,23 @@ def test_kernel_selection_knobs_host_only():
         assert "diagnostic" in lib.hec_encode_kernel_name(1 << 20).decode()
         assert lib.hec_set_kernel_mode(2) != 0
         assert lib.hec_set_host_zero_copy(0) == 0 and lib.hec_set_host_zero_copy(1) == 0
+        assert lib.hec_set_kernel_mode(0) == 0 and lib.hec_set_workgroup_size(256) == 0
+        # the name follows the dispatch predicate: 4 vectors per lane or a grid
+        # cap leave the RS(10,4) fast path for the generic kernel
+        assert lib.hec_set_launch_config(4, 0, 1, 0) == 0
+        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs_apply_kernel<10>")
+        assert lib.hec_set_launch_config(1, 4096, 1, 0) == 0
+        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs_apply_kernel<10>")
+        assert lib.hec_set_launch_config(2, 0, 1, 0) == 0
+        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_bs_encode_kernel")
+        assert lib.hec_set_encode_kernel(0) == 0
+        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_pair_kernel")
+        assert lib.hec_encode_kernel_name(4096).decode().startswith("rs_apply_kernel<10>")
     finally:
         lib.hec_set_kernel_mode(0)
         lib.hec_set_workgroup_size(256)
         lib.hec_set_encode_kernel(1)
+        lib.hec_set_launch_config(1, 0, 1, 0)
 
 
 def test_strided_batch_geometry_checked_before_device():

@@ -174,3 +174,55 @@ def test_randomised_file_geometry_vs_oracle(gpu, tmp_path):
             os.remove(a + H.to_ext(i))
         assert H.rebuild_ec_files(a) == drop
         assert [open(a + H.to_ext(i), "rb").read() for i in range(14)] == want, case
+
+
+def _file_digest(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(16 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def test_production_geometry_multi_slice_multi_job_vs_oracle(gpu, tmp_path):
+    """The file-layer paths a real 30,000 MB volume takes, at a size the C
+    oracle finishes in seconds: 48 MiB large blocks (three 16 MiB slices per
+    large block, ec_files.cpp kLargeSlice), 1 MiB small blocks, 256 KiB
+    buffers (encoder.rs:200-242). .dat = 10 x 48 MiB + 260 MiB + 12,345 B:
+    one large row (remaining > 10 large blocks, encoder.rs:215), then 27
+    small rows = two 25-row GPU jobs; with the large row's 3 slice jobs that
+    is 5 jobs over 3 pipeline slots (out-of-order slot reuse). Shard files are
+    75 MiB = 75 one-MiB rebuild rows = three 25-row rebuild jobs
+    (encoder.rs:244-307). Every shard file is compared with the oracle's."""
+    import helyim_amd as H
+    from oracle import corc
+    MiB = 1 << 20
+    large, small, buf = 48 * MiB, MiB, 256 * 1024
+    size = 10 * large + 260 * MiB + 12345
+    dat = corc.splitmix64_bytes(0x5EED0000 + 48, size)
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    for base in (a, b):
+        with open(base + ".dat", "wb") as f:
+            f.write(memoryview(dat))
+    del dat
+    H.generate_ec_files(a, buf, large, small)
+    assert corc.write_ec_files(b, buf, large, small) == 0
+    want = [_file_digest(b + O.to_ext(i)) for i in range(14)]
+    assert os.path.getsize(a + H.to_ext(0)) == large + 27 * small
+    assert [_file_digest(a + H.to_ext(i)) for i in range(14)] == want
+    os.remove(b + ".dat")
+    # drop 4 (two data, two parity), rebuild on the GPU and in the oracle
+    drop = [2, 7, 10, 13]
+    for i in drop:
+        os.remove(a + H.to_ext(i))
+        os.remove(b + O.to_ext(i))
+    assert H.rebuild_ec_files(a) == drop
+    assert corc.rebuild_ec_files(b) == (0, drop)
+    for i in range(14):
+        assert _file_digest(a + H.to_ext(i)) == want[i] == _file_digest(b + O.to_ext(i)), i
+    # four data shards lost: the decode reads all four parity shards
+    for i in (0, 1, 5, 9):
+        os.remove(a + H.to_ext(i))
+    assert H.rebuild_ec_files(a) == [0, 1, 5, 9]
+    assert [_file_digest(a + H.to_ext(i)) for i in range(14)] == want

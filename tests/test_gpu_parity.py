@@ -602,6 +602,42 @@ def test_ragged_over_launch_limit_is_split(gpu):
     assert torch.equal(t[idx], want)
 
 
+def test_ragged_shard_len_near_4gib(gpu):
+    """One ragged stripe with shard_len = 2^32 - 16 (56 GiB in HBM): the
+    workgroup count is computed in 64 bits (it once wrapped to 0 chunks and
+    left the stripe uncoded without an error). Parity and a 4-erasure rebuild
+    are checked against the C oracle on the first and last 64 KiB of every
+    shard (the columns a wrapped count would have skipped)."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    L, W = (1 << 32) - 16, 1 << 16
+    t = torch.empty(14 * L, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t[:10 * L].view(1, -1), 10 * L, 0x5EED4000)
+    t[10 * L:].zero_()
+    B.encode_ragged(rs, t, [(0, L, L, 0)])
+    torch.cuda.synchronize()
+
+    def cols(lo):
+        return np.stack([t[i * L + lo:i * L + lo + W].cpu().numpy() for i in range(14)])
+
+    heads, tails = cols(0), cols(L - W)
+    for c in (heads, tails):
+        assert np.array_equal(c[10:], corc.encode_stripes(np.ascontiguousarray(c[None, :10]))[0])
+    drop = (0, 3, 11, 13)
+    for i in drop:
+        t[i * L:(i + 1) * L].zero_()
+    mask = 0x3FFF & ~sum(1 << i for i in drop)
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.reconstruct_ragged(rs, t, [(0, L, L, mask)], bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0
+    assert np.array_equal(cols(0), heads) and np.array_equal(cols(L - W), tails)
+    del t
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (12, 4), (8, 8), (1, 1)])
 def test_device_batches_generic_geometry(gpu, k, m):
     """hec_gpu_encode_batch / hec_gpu_reconstruct_batch on geometries other

@@ -642,7 +642,8 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
                          "algorithmic_bytes_per_launch": enc_bytes},
             "encode": {"ms_per_launch": round(enc_ms, 4), "GB_s_hbm": round(enc_gbps, 1),
                        "data_GiB_s": round(S * K_DATA * L / (enc_ms * 1e-3) / 2**30, 1)},
-            "decode": {"ms_per_launch": round(dec_ms, 4), "GB_s_hbm": round(dec_gbps, 1),
+            "decode": {"kernel": H.lib.hec_decode_kernel_name(L).decode(),
+                       "ms_per_launch": round(dec_ms, 4), "GB_s_hbm": round(dec_gbps, 1),
                        "data_GiB_s": round(S * K_DATA * L / (dec_ms * 1e-3) / 2**30, 1),
                        "frac": round(dec_gbps / HBM_PEAK_GBPS, 4),
                        "traffic": prof.get("decode_hbm_bytes_per_launch")},

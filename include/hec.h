@@ -381,6 +381,12 @@ int hec_set_workgroup_size(int threads);
  * XOR program; the default), 0 = table-lookup GF multiply. Both give identical
  * parity (parity-tested); speed only. Returns HEC_OK. */
 int hec_set_encode_kernel(int kind);
+/* RS(10,4) device reconstruct on shard lengths that are a multiple of 8 KiB
+ * (in-place batches): 1 = bit-sliced syndrome decode (the fixed parity
+ * program over the survivors, then an e x e table solve; default), 2 = the
+ * same with a branch instead of the zero page for erased shards, 0 = table
+ * decode of all 10 survivors. Identical bytes (parity-tested); speed only. */
+int hec_set_decode_kernel(int kind);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables
@@ -394,6 +400,8 @@ const char* hec_version(void);
 /* Name of the kernel a 16-byte-aligned RS(10,4) device batch encode of this
  * shard length runs under the current launch configuration (static string). */
 const char* hec_encode_kernel_name(uint64_t shard_len);
+/* Same for a 16-byte-aligned in-place RS(10,4) device batch reconstruct. */
+const char* hec_decode_kernel_name(uint64_t shard_len);
 
 #ifdef __cplusplus
 }

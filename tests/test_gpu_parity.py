@@ -317,6 +317,43 @@ def test_batch_reconstruct_every_pattern(gpu):
     assert torch.equal(t, good)
 
 
+@pytest.mark.parametrize("kind", [1, 2, 0])
+@pytest.mark.parametrize("L", [8192, 3 * 8192])
+def test_decode_kernels_every_pattern(gpu, kind, L):
+    """Every decode kernel (hec_set_decode_kernel: 1 bit-sliced syndrome with
+    the zero page, 2 bit-sliced with branches, 0 table) on 8 KiB-multiple
+    shards: all 1470 patterns (erased slots poisoned), plus an all-present
+    stripe (no-op) and two with too few present (skipped, counted), vs the
+    originals; the kernel-name report follows the switch."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    pats = [c for e in range(1, 5) for c in itertools.combinations(range(14), e)]
+    S = len(pats) + 3
+    t = _stripes(S, L)
+    B.encode_batch(rs, t)
+    good = t.clone()
+    masks = np.full(S, (1 << 14) - 1, dtype=np.int32)
+    for s, p in enumerate(pats):
+        for i in p:
+            t[s, i] = 0xA5
+            masks[s] &= ~(1 << i)
+    masks[-2] = (1 << 14) - 1 - 0b11111           # 9 present
+    masks[-1] = (1 << 14) - 1 - (0b1111 << 10) - 1  # 9 present, all parity gone
+    try:
+        assert H.lib.hec_set_decode_kernel(kind) == 0
+        name = H.lib.hec_decode_kernel_name(L).decode()
+        assert ("bit-sliced" in name) == (kind != 0), name
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda(), bad)
+        torch.cuda.synchronize()
+    finally:
+        H.lib.hec_set_decode_kernel(1)
+    assert int(bad.item()) == 2
+    assert torch.equal(t, good)
+
+
 def test_batch_reconstruct_too_few_present(gpu):
     import torch
     import helyim_amd as H

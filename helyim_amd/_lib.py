@@ -104,6 +104,7 @@ SIGNATURES = {
     "hec_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hec_decode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hec_set_decode_kernel": (_I, [_I]),
+    "hec_set_decode_chunks": (_I, [_I]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

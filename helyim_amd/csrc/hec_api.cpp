@@ -702,6 +702,13 @@ int hec_set_decode_kernel(int kind) {
     return HEC_OK;
 }
 
+int hec_set_decode_chunks(int ranges) {
+    if (ranges != 1 && ranges != 2 && ranges != 4 && ranges != 8)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "decode ranges per workgroup must be 1, 2, 4 or 8");
+    update_launch_config([&](LaunchConfig& c) { c.dec_chunks = ranges; });
+    return HEC_OK;
+}
+
 int hec_set_host_staging(uint64_t max_bytes) {
     host_staging_max() = max_bytes;
     return HEC_OK;

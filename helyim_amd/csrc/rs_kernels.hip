@@ -44,6 +44,9 @@ __device__ __forceinline__ const __attribute__((address_space(4))) T* as_const(c
 #endif
 // Bit-sliced decode: 1 = the selected parity rows are loaded with the data
 // (in flight during the XOR program, more VGPRs); 0 = after the program.
+#ifndef HEC_LOADS_FIRST
+#define HEC_LOADS_FIRST 1
+#endif
 #ifndef HEC_DEC_EARLY_PARITY
 #define HEC_DEC_EARLY_PARITY 1
 #endif
@@ -338,6 +341,12 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
         u32x4 d[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) d[i] = load_full(in_b + uint64_t(in_id[i]) * in_shard + o, true);
+#if HEC_LOADS_FIRST
+        // all ten loads in flight before any math: without this fence the
+        // scheduler interleaves them with the table multiply two at a time
+        // (36 VGPRs, but one wave then waits on HBM five times per chunk)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         if constexpr (XORONLY) {
 #pragma unroll
             for (int i = 0; i < K; ++i) mac<R, true>(acc, d[i], tab + i * (R * 5));
@@ -593,33 +602,56 @@ __device__ __forceinline__ void rs104_bs_dec_chunk(uint8_t* b, uint64_t shard, u
         }
 }
 
-template <int TB, bool ZP>
+// CPW consecutive column ranges of one stripe per workgroup: the stripe's
+// mask and tables are loaded once and the dependent-load latency at the
+// start of a workgroup (mask -> LUT -> addresses / tables) is paid once per
+// CPW ranges (a compiled-in mask measured the bare cost: 1.4% on a
+// parity-only batch, tools/decode_pattern_probe.py).
+template <int TB, bool ZP, int CPW>
 __global__ __launch_bounds__(TB) void rs104_bs_decode_kernel(ApplyArgs a) {
     const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
-    const uint32_t stripe = item / a.chunks_per_stripe;
-    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
+    const uint32_t groups = a.chunks_per_stripe / CPW;
+    const uint32_t stripe = item / groups;
+    const uint32_t g = item - stripe * groups;
+#ifdef HEC_DEC_PROBE_MASK  // measurement variant: a compile-time mask, no dependent mask load
+    const uint32_t mask = HEC_DEC_PROBE_MASK;
+#else
     const uint32_t mask = as_const(a.masks)[stripe] & 0x3FFFu;
+#endif
     const uint32_t present = __builtin_popcount(mask);
     if (present < 10) {
-        if (chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
+        if (g == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
         return;
     }
     if (present == 14) return;  // upstream: all present -> no-op
     cu32p syn = as_const(a.syn) + as_const(a.lut)[mask] * uint32_t(kSynWords);
-    rs104_bs_dec_chunk<TB, ZP>(a.out_base + uint64_t(stripe) * a.out_stripe, a.out_shard, chunk, mask, syn, a.zero);
+    uint8_t* b = a.out_base + uint64_t(stripe) * a.out_stripe;
+#pragma unroll 1
+    for (int c = 0; c < CPW; ++c) rs104_bs_dec_chunk<TB, ZP>(b, a.out_shard, g * CPW + c, mask, syn, a.zero);
 }
 
-template <int TB, bool ZP>
+template <int TB, bool ZP, int CPW>
 static hipError_t launch_rs104_bs_dec(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
     const uint64_t chunk = uint64_t(TB) * 2 * kVecBytes;
     a.chunks_per_stripe = uint32_t(a.len / chunk);
-    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
+    if (a.chunks_per_stripe % CPW != 0) return launch_rs104_bs_dec<TB, ZP, 1>(a, cfg, stream);
+    a.n_items = uint64_t(a.chunks_per_stripe / CPW) * a.n_stripes;
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs104_bs_decode_kernel<TB, ZP>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
+    hipLaunchKernelGGL((rs104_bs_decode_kernel<TB, ZP, CPW>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
     return hipGetLastError();
+}
+
+template <int TB, bool ZP>
+static hipError_t launch_rs104_bs_dec_cpw(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
+    switch (cfg.dec_chunks) {
+        case 2: return launch_rs104_bs_dec<TB, ZP, 2>(a, cfg, stream);
+        case 4: return launch_rs104_bs_dec<TB, ZP, 4>(a, cfg, stream);
+        case 8: return launch_rs104_bs_dec<TB, ZP, 8>(a, cfg, stream);
+        default: return launch_rs104_bs_dec<TB, ZP, 1>(a, cfg, stream);
+    }
 }
 
 // Ragged encode with every stripe length a multiple of 8 KiB: workgroup ->
@@ -824,8 +856,8 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
     }
     if (a.fast104 && aligned && rs104_fast_ok(a.len, cfg) && items <= kMaxLaunchBlocks) {
         if (a.masks && rs104_bs_decode_ok(a, cfg))
-            return cfg.bs_decode == 2 ? launch_rs104_bs_dec<kThreads, false>(a, cfg, stream)
-                                      : launch_rs104_bs_dec<kThreads, true>(a, cfg, stream);
+            return cfg.bs_decode == 2 ? launch_rs104_bs_dec_cpw<kThreads, false>(a, cfg, stream)
+                                      : launch_rs104_bs_dec_cpw<kThreads, true>(a, cfg, stream);
         if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, cfg, stream)
                                           : launch_rs104<true, false>(a, cfg, stream);
         if (rs104_bitslice_ok(a.len, cfg)) return launch_rs104_bs_cfg(a, cfg, stream);

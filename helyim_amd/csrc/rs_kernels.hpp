@@ -102,6 +102,8 @@ struct LaunchConfig {
     int bs_decode = 1;           // RS(10,4) device decode on 8 KiB-multiple shards: 1 = bit-sliced
                                  // syndrome kernel, erased data read from a zero page (default);
                                  // 2 = same, branch around erased loads; 0 = table kernel (speed only)
+    int dec_chunks = 1;          // bit-sliced decode: 8 KiB column ranges per workgroup (1, 2, 4, 8;
+                                 // ranges of one stripe, speed only)
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
                                  // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
                                  // multiply (speed only)

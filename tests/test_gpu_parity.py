@@ -317,9 +317,9 @@ def test_batch_reconstruct_every_pattern(gpu):
     assert torch.equal(t, good)
 
 
-@pytest.mark.parametrize("kind", [1, 2, 0])
-@pytest.mark.parametrize("L", [8192, 3 * 8192])
-def test_decode_kernels_every_pattern(gpu, kind, L):
+@pytest.mark.parametrize("kind,cpw", [(1, 1), (1, 2), (1, 4), (1, 8), (2, 1), (2, 4), (0, 1)])
+@pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192])
+def test_decode_kernels_every_pattern(gpu, kind, cpw, L):
     """Every decode kernel (hec_set_decode_kernel: 1 bit-sliced syndrome with
     the zero page, 2 bit-sliced with branches, 0 table) on 8 KiB-multiple
     shards: all 1470 patterns (erased slots poisoned), plus an all-present
@@ -343,6 +343,7 @@ def test_decode_kernels_every_pattern(gpu, kind, L):
     masks[-1] = (1 << 14) - 1 - (0b1111 << 10) - 1  # 9 present, all parity gone
     try:
         assert H.lib.hec_set_decode_kernel(kind) == 0
+        assert H.lib.hec_set_decode_chunks(cpw) == 0  # ranges per workgroup (falls back when L does not divide)
         name = H.lib.hec_decode_kernel_name(L).decode()
         assert ("bit-sliced" in name) == (kind != 0), name
         bad = torch.zeros(1, dtype=torch.int32, device="cuda")
@@ -350,6 +351,7 @@ def test_decode_kernels_every_pattern(gpu, kind, L):
         torch.cuda.synchronize()
     finally:
         H.lib.hec_set_decode_kernel(1)
+        H.lib.hec_set_decode_chunks(1)
     assert int(bad.item()) == 2
     assert torch.equal(t, good)
 

@@ -1,0 +1,76 @@
+"""Decode rate vs erasure pattern on the BASELINE batch (4096 x 1 MiB,
+device-resident): is the decode/encode gap the arithmetic or where the
+erased shards sit? Same-pattern batches ({10..13} is an encode in disguise:
+read data 0-9, write parity 10-13) against the bench's random 4-erasure
+patterns, for each decode kernel, interleaved rounds in one process, with the
+encode of the same batch as the reference line.
+
+python tools/decode_pattern_probe.py [--rounds 7] [--decs 0,1]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--shard-len", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--decs", default="0,1")
+    ap.add_argument("--cpws", default="1", help="bit-sliced decode: 8 KiB ranges per workgroup")
+    args = ap.parse_args()
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    import bench
+    S, L = args.stripes, args.shard_len
+    rs = H.ReedSolomon(10, 4)
+    t = torch.empty((S, 14, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t, 10 * L, 0x5EED0000)
+    B.encode_batch(rs, t)
+    full = (1 << 14) - 1
+
+    def fixed(drop):
+        return np.full(S, full & ~sum(1 << i for i in drop), np.int32)
+
+    pats = {"random4": bench.erasure_masks(S, 0), "p10-13": fixed((10, 11, 12, 13)),
+            "d0-3": fixed((0, 1, 2, 3)), "d6-9": fixed((6, 7, 8, 9)), "0,5,10,13": fixed((0, 5, 10, 13)),
+            "d0,d9,p10": fixed((0, 9, 10)), "one_d4": fixed((4,))}
+    masks = {k: torch.from_numpy(v).cuda() for k, v in pats.items()}
+    decs = [(int(x), int(c)) for x in args.decs.split(",") for c in args.cpws.split(",")]
+    res = {}
+    s = torch.cuda.current_stream()
+    for _ in range(args.rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        B.encode_batch(rs, t)
+        e1.record(s)
+        torch.cuda.synchronize()
+        res.setdefault(("encode", -1), []).append(e0.elapsed_time(e1))
+        for k, m in masks.items():
+            for d in decs:
+                H.lib.hec_set_decode_kernel(d[0])
+                H.lib.hec_set_decode_chunks(d[1])
+                e0.record(s)
+                B.reconstruct_batch(rs, t, m)
+                e1.record(s)
+                torch.cuda.synchronize()
+                res.setdefault((k, d), []).append(e0.elapsed_time(e1))
+    H.lib.hec_set_decode_kernel(1)
+    H.lib.hec_set_decode_chunks(1)
+    for (k, d), v in res.items():
+        e = 4 if k in ("random4", "p10-13", "d0-3", "d6-9", "0,5,10,13") else (3 if k == "d0,d9,p10" else 1)
+        nbytes = S * (10 + e) * L if k != "encode" else S * 14 * L
+        ms = float(np.median(v))
+        print(json.dumps({"pattern": k, "decode_kernel": d, "lib": os.path.basename(H.LIB_PATH), "ms_med": round(ms, 3),
+                          "GB_s": round(nbytes / ms / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -103,8 +103,6 @@ SIGNATURES = {
     "hec_host_numa_node": (_I, [_P, ctypes.POINTER(_I)]),
     "hec_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hec_decode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
-    "hec_set_decode_kernel": (_I, [_I]),
-    "hec_set_decode_chunks": (_I, [_I]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

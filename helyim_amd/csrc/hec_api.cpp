@@ -196,13 +196,6 @@ int DevicePlanSet::upload(const HostPlans& hp, const std::vector<uint32_t>* lut_
     if ((rc = grow_upload(tabs, cap_tabs, hp.tabs.data(), hp.tabs.size(), s))) return rc;
     if ((rc = grow_upload(idx, cap_idx, hp.idx.data(), hp.idx.size(), s))) return rc;
     if (lut_host && (rc = grow_upload(lut, cap_lut, lut_host->data(), lut_host->size(), s))) return rc;
-    if (!hp.syn.empty()) {
-        if ((rc = grow_upload(syn, cap_syn, hp.syn.data(), hp.syn.size(), s))) return rc;
-        if (!zero) {
-            HEC_HIP(hipMalloc(reinterpret_cast<void**>(&zero), kZeroPageBytes));
-            HEC_HIP(hipMemsetAsync(zero, 0, kZeroPageBytes, s));
-        }
-    }
     // Host vectors may be freed by the caller right after: make the copies land.
     HEC_HIP(hipStreamSynchronize(s));
     return HEC_OK;
@@ -213,12 +206,9 @@ void DevicePlanSet::release() {
     (void)hipFree(tabs);
     (void)hipFree(idx);
     (void)hipFree(lut);
-    (void)hipFree(syn);
-    (void)hipFree(zero);
     plans = nullptr;
-    tabs = idx = lut = syn = nullptr;
-    zero = nullptr;
-    cap_plans = cap_tabs = cap_idx = cap_lut = cap_syn = 0;
+    tabs = idx = lut = nullptr;
+    cap_plans = cap_tabs = cap_idx = cap_lut = 0;
 }
 
 // upstream reconstruct_internal: first k present shards -> sub-matrix ->
@@ -306,42 +296,6 @@ int geom_device(const hec_rs* rs, GeomDevice** out) {
     return HEC_OK;
 }
 
-// Tables of the bit-sliced syndrome decode (bitslice_decode.hpp) for one
-// RS(10,4) present mask with 10..13 shards present. The selected parity rows
-// are the first e_d present ones -- with every present data shard, exactly
-// the first 10 present shards upstream reconstruct inverts
-// (reed-solomon-erasure 6.0.0 reconstruct_internal, encoder.rs:288) -- so the
-// solution is upstream's, byte for byte.
-int syndrome_tables(const hec_rs* rs, uint32_t mask, uint32_t out[kSynWords]) {
-    const int K = 10;
-    const Gf& g = gf();
-    std::fill(out, out + kSynWords, 0u);
-    std::vector<int> ed, sel;
-    for (int i = 0; i < K; ++i)
-        if (!((mask >> i) & 1)) ed.push_back(i);
-    for (int j = 0; j < 4 && sel.size() < ed.size(); ++j)
-        if ((mask >> (K + j)) & 1) sel.push_back(j);
-    const int e = int(ed.size());
-    if (e == 0) return HEC_OK;  // parity only: P'_j is the parity
-    if (int(sel.size()) != e) return fail(HEC_ERR_TOO_FEW_SHARDS_PRESENT, "syndrome tables");
-    Mat sub(e, e), inv;
-    for (int t = 0; t < e; ++t)
-        for (int u = 0; u < e; ++u) sub.at(t, u) = rs->matrix.at(K + sel[t], ed[u]);
-    if (!mat_invert(sub, inv)) return fail(HEC_ERR_INVALID_ARGUMENT, "singular syndrome block");
-    auto put = [&](int row, int j, uint8_t c) { perm_tables(c, out + (row * 4 + j) * kTabWords); };
-    for (int r = 0; r < e; ++r)
-        for (int t = 0; t < e; ++t) put(r, sel[t], inv.at(r, t));
-    for (int j = 0; j < 4; ++j) {
-        if ((mask >> (K + j)) & 1) continue;  // only erased parity rows are written
-        for (int t = 0; t < e; ++t) {
-            uint8_t c = 0;
-            for (int u = 0; u < e; ++u) c ^= g.mul[rs->matrix.at(K + j, ed[u])][inv.at(u, t)];
-            put(4 + j, sel[t], c);
-        }
-    }
-    return HEC_OK;
-}
-
 int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_geom_mu);
     if (gd->decode_ready) return HEC_OK;
@@ -352,7 +306,6 @@ int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
     if (is104) hp.fixed_rows = 4;
     std::vector<uint32_t> lut(size_t(1) << n, kNoPlan);
     const uint32_t noop = hp.add_noop(uint32_t(k));
-    if (is104) hp.syn.assign(kSynWords, 0u);  // no-op plan
     uint8_t present[16];
     Mat coefs;
     std::vector<uint32_t> in_ids, out_ids;
@@ -368,11 +321,6 @@ int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
         int rc = decode_plan(rs, present, false, coefs, in_ids, out_ids, &is_noop);
         if (rc) return rc;
         lut[mask] = hp.add(coefs, in_ids, out_ids);
-        if (is104) {
-            uint32_t t[kSynWords];
-            if ((rc = syndrome_tables(rs, mask, t))) return rc;
-            hp.syn.insert(hp.syn.end(), t, t + kSynWords);
-        }
     }
     int rc = gd->decode_dense.upload(hp, &lut, s);
     if (rc) return rc;
@@ -402,8 +350,6 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
     a.lut = ps.lut;
     a.bad_count = bad;
     a.fast104 = ps.fast104 ? 1u : 0u;
-    a.syn = ps.syn;
-    a.zero = ps.zero;
     a.mask_limit = ps.lut_bits ? ((1u << ps.lut_bits) - 1u) : 0u;
     if (masks && !ps.lut) return fail(HEC_ERR_INVALID_ARGUMENT, "per-stripe masks need a decode LUT");
     const uint64_t align = uint64_t(reinterpret_cast<uintptr_t>(in_base)) | in_stripe | in_shard |
@@ -693,19 +639,6 @@ int hec_set_workgroup_size(int threads) {
 int hec_set_encode_kernel(int kind) {
     if (kind != 0 && kind != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0 or 1");
     update_launch_config([&](LaunchConfig& c) { c.bitslice = kind; });
-    return HEC_OK;
-}
-
-int hec_set_decode_kernel(int kind) {
-    if (kind < 0 || kind > 2) return fail(HEC_ERR_INVALID_ARGUMENT, "decode kernel must be 0, 1 or 2");
-    update_launch_config([&](LaunchConfig& c) { c.bs_decode = kind; });
-    return HEC_OK;
-}
-
-int hec_set_decode_chunks(int ranges) {
-    if (ranges != 1 && ranges != 2 && ranges != 4 && ranges != 8)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "decode ranges per workgroup must be 1, 2, 4 or 8");
-    update_launch_config([&](LaunchConfig& c) { c.dec_chunks = ranges; });
     return HEC_OK;
 }
 

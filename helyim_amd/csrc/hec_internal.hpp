@@ -71,9 +71,6 @@ struct HostPlans {
     // > 0: every plan (no-ops included) gets exactly nin * fixed_rows table
     // rows, so plan p's tables start at p * nin * fixed_rows * kTabWords.
     uint32_t fixed_rows = 0;
-    // RS(10,4) dense decode only: kSynWords syndrome-decode words per plan
-    // (bitslice_decode.hpp), plan p at p * kSynWords.
-    std::vector<uint32_t> syn;
     // Append a plan: out rows = coefs (nout x nin) over inputs in_ids.
     uint32_t add(const Mat& coefs, const std::vector<uint32_t>& in_ids,
                  const std::vector<uint32_t>& out_ids);
@@ -86,19 +83,12 @@ struct DevicePlanSet {
     uint32_t* tabs = nullptr;
     uint32_t* idx = nullptr;
     uint32_t* lut = nullptr;
-    uint32_t* syn = nullptr;   // syndrome tables (HostPlans::syn), RS(10,4) decode set only
-    uint8_t* zero = nullptr;   // kZeroPageBytes of zeros, allocated with syn
-    size_t cap_plans = 0, cap_tabs = 0, cap_idx = 0, cap_lut = 0, cap_syn = 0;
+    size_t cap_plans = 0, cap_tabs = 0, cap_idx = 0, cap_lut = 0;
     bool fast104 = false;  // RS(10,4) set with fixed 4-row tables (rs104_kernel eligible)
     uint32_t lut_bits = 0; // total shards the LUT covers (2^lut_bits entries)
     int upload(const HostPlans& hp, const std::vector<uint32_t>* lut_host, hipStream_t s);
     void release();
 };
-
-// Zero page read by the bit-sliced decode in place of erased data shards
-// (one 2 x 256 x 16-byte column range, doubled for headroom).
-constexpr size_t kZeroPageBytes = 16384;
-int syndrome_tables(const hec_rs* rs, uint32_t mask, uint32_t out[kSynWords]);
 
 // Decode plan of one erasure pattern (upstream reconstruct semantics).
 // present: n flags. data_only: skip missing parity. Returns HEC_OK or

@@ -21,7 +21,6 @@
 
 #include "rs_kernels.hpp"
 #include "bitslice.hpp"
-#include "bitslice_decode.hpp"
 
 namespace hec {
 
@@ -44,11 +43,10 @@ __device__ __forceinline__ const __attribute__((address_space(4))) T* as_const(c
 #endif
 // Bit-sliced decode: 1 = the selected parity rows are loaded with the data
 // (in flight during the XOR program, more VGPRs); 0 = after the program.
+// Table kernels: 1 = all ten shard loads issued before the math (the
+// shipped form; 0 = the scheduler's interleaving, a measurement variant).
 #ifndef HEC_LOADS_FIRST
 #define HEC_LOADS_FIRST 1
-#endif
-#ifndef HEC_DEC_EARLY_PARITY
-#define HEC_DEC_EARLY_PARITY 1
 #endif
 
 // Global-address-space views: the nontemporal hint on a flat (generic)
@@ -517,143 +515,6 @@ __global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
                        a.in_shard, a.out_shard, chunk);
 }
 
-// ---------------------------------------------------------------------------
-// Bit-sliced RS(10,4) syndrome decode (bitslice_decode.hpp): the lane layout
-// of the bit-sliced encode (32 bytes of every shard per lane, two 16-byte
-// vectors TB*16 apart). A lane loads exactly the stripe's 10 survivors: the
-// present data shards and the selected parity rows. Erased data shards read
-// as zero: from a zeroed 8 KiB device page (ZP, straight-line loads; the page
-// stays cache resident, no HBM traffic) or by a uniform branch around the
-// load (!ZP). Decoded in place; writes exactly the erased shards.
-// ---------------------------------------------------------------------------
-template <int TB, bool ZP>
-__device__ __forceinline__ void rs104_bs_dec_chunk(uint8_t* b, uint64_t shard, uint32_t chunk, uint32_t mask,
-                                                   cu32p syn, const uint8_t* zero) {
-    constexpr int K = 10, R = 4;
-    const uint64_t o0 = uint64_t(chunk) * (TB * 2 * kVecBytes) + threadIdx.x * kVecBytes;
-    const uint64_t o1 = o0 + TB * kVecBytes;
-    const uint8_t* z0 = zero + threadIdx.x * kVecBytes;
-    const uint8_t* z1 = z0 + TB * kVecBytes;
-    const uint32_t erased = ~mask & 0x3FFFu;
-    const uint32_t ed = __builtin_popcount(erased & 0x3FFu);
-    const uint32_t sel = syn_selected(mask, ed);
-    const u32x4 zv = u32x4{0, 0, 0, 0};
-    // shard i's two vectors; erased data shards read as zero, unselected
-    // parity rows are not needed (zero)
-    auto load2 = [&](int i, bool use, u32x4& v0, u32x4& v1) {
-        if constexpr (ZP) {
-            v0 = load_full(use ? b + uint64_t(i) * shard + o0 : z0, true);
-            v1 = load_full(use ? b + uint64_t(i) * shard + o1 : z1, true);
-        } else {
-            if (use) {
-                v0 = load_full(b + uint64_t(i) * shard + o0, true);
-                v1 = load_full(b + uint64_t(i) * shard + o1, true);
-            } else {
-                v0 = zv;
-                v1 = zv;
-            }
-        }
-    };
-    u32x4 d[K][2], pv[R][2];
-#pragma unroll
-    for (int i = 0; i < K; ++i) load2(i, ((mask >> i) & 1u) != 0, d[i][0], d[i][1]);
-#if HEC_DEC_EARLY_PARITY
-#pragma unroll
-    for (int j = 0; j < R; ++j) load2(K + j, ((sel >> j) & 1u) != 0, pv[j][0], pv[j][1]);
-#endif
-    uint32_t p[K * 8], pp[R * 8], dd[R * 8], q[R * 8];
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            p[8 * i + w] = d[i][0][w];
-            p[8 * i + 4 + w] = d[i][1][w];
-        }
-    rs104_syndrome_phase1(p, mask, sel, q);
-#if !HEC_DEC_EARLY_PARITY
-#pragma unroll
-    for (int j = 0; j < R; ++j) load2(K + j, ((sel >> j) & 1u) != 0, pv[j][0], pv[j][1]);
-#endif
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            pp[8 * j + w] = pv[j][0][w];
-            pp[8 * j + 4 + w] = pv[j][1][w];
-        }
-    rs104_syndrome_phase2(q, pp, mask, ed, sel, syn, dd);
-    uint32_t e = erased & 0x3FFu;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {  // erased data shards, ascending
-        if (uint32_t(r) >= ed) break;
-        const uint32_t id = __builtin_ctz(e);
-        e &= e - 1;
-        store_full(b + uint64_t(id) * shard + o0, u32x4{dd[8 * r], dd[8 * r + 1], dd[8 * r + 2], dd[8 * r + 3]}, true);
-        store_full(b + uint64_t(id) * shard + o1, u32x4{dd[8 * r + 4], dd[8 * r + 5], dd[8 * r + 6], dd[8 * r + 7]},
-                   true);
-    }
-#pragma unroll
-    for (int j = 0; j < R; ++j)  // erased parity rows
-        if ((erased >> (K + j)) & 1u) {
-            store_full(b + uint64_t(K + j) * shard + o0, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]},
-                       true);
-            store_full(b + uint64_t(K + j) * shard + o1,
-                       u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]}, true);
-        }
-}
-
-// CPW consecutive column ranges of one stripe per workgroup: the stripe's
-// mask and tables are loaded once and the dependent-load latency at the
-// start of a workgroup (mask -> LUT -> addresses / tables) is paid once per
-// CPW ranges (a compiled-in mask measured the bare cost: 1.4% on a
-// parity-only batch, tools/decode_pattern_probe.py).
-template <int TB, bool ZP, int CPW>
-__global__ __launch_bounds__(TB) void rs104_bs_decode_kernel(ApplyArgs a) {
-    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
-    const uint32_t groups = a.chunks_per_stripe / CPW;
-    const uint32_t stripe = item / groups;
-    const uint32_t g = item - stripe * groups;
-#ifdef HEC_DEC_PROBE_MASK  // measurement variant: a compile-time mask, no dependent mask load
-    const uint32_t mask = HEC_DEC_PROBE_MASK;
-#else
-    const uint32_t mask = as_const(a.masks)[stripe] & 0x3FFFu;
-#endif
-    const uint32_t present = __builtin_popcount(mask);
-    if (present < 10) {
-        if (g == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
-        return;
-    }
-    if (present == 14) return;  // upstream: all present -> no-op
-    cu32p syn = as_const(a.syn) + as_const(a.lut)[mask] * uint32_t(kSynWords);
-    uint8_t* b = a.out_base + uint64_t(stripe) * a.out_stripe;
-#pragma unroll 1
-    for (int c = 0; c < CPW; ++c) rs104_bs_dec_chunk<TB, ZP>(b, a.out_shard, g * CPW + c, mask, syn, a.zero);
-}
-
-template <int TB, bool ZP, int CPW>
-static hipError_t launch_rs104_bs_dec(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(TB) * 2 * kVecBytes;
-    a.chunks_per_stripe = uint32_t(a.len / chunk);
-    if (a.chunks_per_stripe % CPW != 0) return launch_rs104_bs_dec<TB, ZP, 1>(a, cfg, stream);
-    a.n_items = uint64_t(a.chunks_per_stripe / CPW) * a.n_stripes;
-    if (a.n_items == 0) return hipSuccess;
-    a.xcd_remap = uint32_t(cfg.xcd_remap);
-    a.xcd_parts = uint32_t(cfg.xcd_parts);
-    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs104_bs_decode_kernel<TB, ZP, CPW>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
-    return hipGetLastError();
-}
-
-template <int TB, bool ZP>
-static hipError_t launch_rs104_bs_dec_cpw(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
-    switch (cfg.dec_chunks) {
-        case 2: return launch_rs104_bs_dec<TB, ZP, 2>(a, cfg, stream);
-        case 4: return launch_rs104_bs_dec<TB, ZP, 4>(a, cfg, stream);
-        case 8: return launch_rs104_bs_dec<TB, ZP, 8>(a, cfg, stream);
-        default: return launch_rs104_bs_dec<TB, ZP, 1>(a, cfg, stream);
-    }
-}
-
 // Ragged encode with every stripe length a multiple of 8 KiB: workgroup ->
 // stripe map as rs104_ragged_kernel, one 8 KiB column range per workgroup.
 __global__ __launch_bounds__(kThreads) void rs104_bs_ragged_kernel(RaggedArgs a) {
@@ -805,21 +666,9 @@ static bool rs104_bitslice_ok(uint64_t len, const LaunchConfig& cfg) {
     return cfg.bitslice && cfg.mode == 0 && len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0;
 }
 
-// Bit-sliced syndrome decode: GF mode, the RS(10,4) syndrome tables and zero
-// page present, in-place layout, shard length a multiple of 8 KiB (256-thread
-// workgroups; the zero page holds one 8 KiB column range).
-static bool rs104_bs_decode_ok(const ApplyArgs& a, const LaunchConfig& cfg) {
-    return cfg.bs_decode != 0 && cfg.mode == 0 && a.syn && a.zero && a.in_base == a.out_base &&
-           a.in_shard == a.out_shard && a.in_stripe == a.out_stripe &&
-           a.len % (2 * uint64_t(kThreads) * kVecBytes) == 0;
-}
-
 const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
     if (!rs104_fast_ok(len, cfg)) return "rs_apply_kernel<10> (table lookup)";
     if (cfg.mode == 1) return "rs104_kernel<DEC=true, XORONLY=true> (diagnostic)";
-    if (cfg.bs_decode != 0 && len % (2 * uint64_t(kThreads) * kVecBytes) == 0)
-        return cfg.bs_decode == 2 ? "rs104_bs_decode_kernel<ZP=false> (bit-sliced syndrome)"
-                                  : "rs104_bs_decode_kernel<ZP=true> (bit-sliced syndrome)";
     if (cfg.vec_per_thread == 2) return "rs104_pair_kernel<DEC=true> (table lookup)";
     return "rs104_kernel<DEC=true> (table lookup)";
 }
@@ -855,9 +704,6 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
         return hipSuccess;
     }
     if (a.fast104 && aligned && rs104_fast_ok(a.len, cfg) && items <= kMaxLaunchBlocks) {
-        if (a.masks && rs104_bs_decode_ok(a, cfg))
-            return cfg.bs_decode == 2 ? launch_rs104_bs_dec_cpw<kThreads, false>(a, cfg, stream)
-                                      : launch_rs104_bs_dec_cpw<kThreads, true>(a, cfg, stream);
         if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, cfg, stream)
                                           : launch_rs104<true, false>(a, cfg, stream);
         if (rs104_bitslice_ok(a.len, cfg)) return launch_rs104_bs_cfg(a, cfg, stream);

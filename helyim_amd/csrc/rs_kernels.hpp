@@ -26,9 +26,6 @@ constexpr int kThreads = 256;               // 4 waves of 64 lanes
 // 4x larger chunks) keeps every launch legal.
 constexpr uint64_t kMaxLaunchBlocks = 1ull << 23;
 constexpr int kVecBytes = 16;               // one dwordx4 per lane per access
-// Syndrome-decode table words per RS(10,4) erasure pattern: 8 output rows x 4
-// syndromes x 5 v_perm table words (bitslice_decode.hpp).
-constexpr int kSynWords = 8 * 4 * 5;
 
 struct ApplyArgs {
     const uint8_t* in_base;      // input shard (stripe s, id i) = in_base + s*in_stripe + i*in_shard
@@ -53,9 +50,6 @@ struct ApplyArgs {
     uint32_t chunk_rot;          // 1: rotate each stripe's chunk order by a hash of the stripe id
     uint32_t fast104;            // 1: RS(10,4) plan set with 4-row tables; encode = plan 0 at
                                  //    offset 0, decode = tables at lut[mask] * 200 words
-    const uint32_t* syn;         // RS(10,4) decode: syndrome tables at lut[mask] * kSynWords
-                                 //    (bitslice_decode.hpp), or null
-    const uint8_t* zero;         // >= 8 KiB of zeros in device memory (bit-sliced decode)
 };
 
 // Ragged RS(10,4) batch (every stripe its own length / stride / mask); all
@@ -99,11 +93,6 @@ struct LaunchConfig {
     int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
     int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
     int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
-    int bs_decode = 1;           // RS(10,4) device decode on 8 KiB-multiple shards: 1 = bit-sliced
-                                 // syndrome kernel, erased data read from a zero page (default);
-                                 // 2 = same, branch around erased loads; 0 = table kernel (speed only)
-    int dec_chunks = 1;          // bit-sliced decode: 8 KiB column ranges per workgroup (1, 2, 4, 8;
-                                 // ranges of one stripe, speed only)
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
                                  // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
                                  // multiply (speed only)

@@ -381,16 +381,6 @@ int hec_set_workgroup_size(int threads);
  * XOR program; the default), 0 = table-lookup GF multiply. Both give identical
  * parity (parity-tested); speed only. Returns HEC_OK. */
 int hec_set_encode_kernel(int kind);
-/* RS(10,4) device reconstruct on shard lengths that are a multiple of 8 KiB
- * (in-place batches): 1 = bit-sliced syndrome decode (the fixed parity
- * program over the survivors, then an e x e table solve; default), 2 = the
- * same with a branch instead of the zero page for erased shards, 0 = table
- * decode of all 10 survivors. Identical bytes (parity-tested); speed only. */
-int hec_set_decode_kernel(int kind);
-/* Bit-sliced decode: consecutive 8 KiB column ranges of one stripe per
- * workgroup (1, 2, 4 or 8), so the stripe's mask and tables are fetched once
- * per workgroup. Speed only. */
-int hec_set_decode_chunks(int ranges);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables

@@ -317,14 +317,14 @@ def test_batch_reconstruct_every_pattern(gpu):
     assert torch.equal(t, good)
 
 
-@pytest.mark.parametrize("kind,cpw", [(1, 1), (1, 2), (1, 4), (1, 8), (2, 1), (2, 4), (0, 1)])
-@pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192])
-def test_decode_kernels_every_pattern(gpu, kind, cpw, L):
-    """Every decode kernel (hec_set_decode_kernel: 1 bit-sliced syndrome with
-    the zero page, 2 bit-sliced with branches, 0 table) on 8 KiB-multiple
-    shards: all 1470 patterns (erased slots poisoned), plus an all-present
-    stripe (no-op) and two with too few present (skipped, counted), vs the
-    originals; the kernel-name report follows the switch."""
+@pytest.mark.parametrize("vec", [1, 2])
+@pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192 + 16])
+def test_decode_kernels_every_pattern(gpu, vec, L):
+    """The RS(10,4) decode kernels (one 4 KiB chunk per workgroup, or the
+    pair kernel's two) with all ten loads issued before the math: all 1470
+    patterns (erased slots poisoned), plus an all-present stripe (no-op) and
+    two with too few present (skipped, counted), vs the originals; the
+    kernel-name report follows the launch configuration."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -342,16 +342,14 @@ def test_decode_kernels_every_pattern(gpu, kind, cpw, L):
     masks[-2] = (1 << 14) - 1 - 0b11111           # 9 present
     masks[-1] = (1 << 14) - 1 - (0b1111 << 10) - 1  # 9 present, all parity gone
     try:
-        assert H.lib.hec_set_decode_kernel(kind) == 0
-        assert H.lib.hec_set_decode_chunks(cpw) == 0  # ranges per workgroup (falls back when L does not divide)
+        B.set_launch_config(vec_per_thread=vec)
         name = H.lib.hec_decode_kernel_name(L).decode()
-        assert ("bit-sliced" in name) == (kind != 0), name
+        assert ("pair" in name) == (vec == 2 and L % 8192 == 0), name
         bad = torch.zeros(1, dtype=torch.int32, device="cuda")
         B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda(), bad)
         torch.cuda.synchronize()
     finally:
-        H.lib.hec_set_decode_kernel(1)
-        H.lib.hec_set_decode_chunks(1)
+        B.set_launch_config()
     assert int(bad.item()) == 2
     assert torch.equal(t, good)
 

@@ -2,10 +2,12 @@
 device-resident): is the decode/encode gap the arithmetic or where the
 erased shards sit? Same-pattern batches ({10..13} is an encode in disguise:
 read data 0-9, write parity 10-13) against the bench's random 4-erasure
-patterns, for each decode kernel, interleaved rounds in one process, with the
-encode of the same batch as the reference line.
+patterns, per launch configuration (vectors per lane: 1 = one 4 KiB chunk per
+workgroup, 2 = the pair kernel), interleaved rounds in one process, with the
+encode of the same batch as the reference line. HEC_LIB_PATH selects a
+measurement build (Makefile VARIANTS).
 
-python tools/decode_pattern_probe.py [--rounds 7] [--decs 0,1]
+python tools/decode_pattern_probe.py [--rounds 7] [--vecs 1,2]
 """
 import argparse
 import json
@@ -22,8 +24,7 @@ def main():
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--shard-len", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--decs", default="0,1")
-    ap.add_argument("--cpws", default="1", help="bit-sliced decode: 8 KiB ranges per workgroup")
+    ap.add_argument("--vecs", default="1", help="16-byte vectors per lane (hec_set_launch_config)")
     args = ap.parse_args()
     import torch
     import helyim_amd as H
@@ -43,7 +44,7 @@ def main():
             "d0-3": fixed((0, 1, 2, 3)), "d6-9": fixed((6, 7, 8, 9)), "0,5,10,13": fixed((0, 5, 10, 13)),
             "d0,d9,p10": fixed((0, 9, 10)), "one_d4": fixed((4,))}
     masks = {k: torch.from_numpy(v).cuda() for k, v in pats.items()}
-    decs = [(int(x), int(c)) for x in args.decs.split(",") for c in args.cpws.split(",")]
+    decs = [int(x) for x in args.vecs.split(",")]
     res = {}
     s = torch.cuda.current_stream()
     for _ in range(args.rounds):
@@ -55,20 +56,18 @@ def main():
         res.setdefault(("encode", -1), []).append(e0.elapsed_time(e1))
         for k, m in masks.items():
             for d in decs:
-                H.lib.hec_set_decode_kernel(d[0])
-                H.lib.hec_set_decode_chunks(d[1])
+                B.set_launch_config(vec_per_thread=d)
                 e0.record(s)
                 B.reconstruct_batch(rs, t, m)
                 e1.record(s)
                 torch.cuda.synchronize()
                 res.setdefault((k, d), []).append(e0.elapsed_time(e1))
-    H.lib.hec_set_decode_kernel(1)
-    H.lib.hec_set_decode_chunks(1)
+    B.set_launch_config()
     for (k, d), v in res.items():
         e = 4 if k in ("random4", "p10-13", "d0-3", "d6-9", "0,5,10,13") else (3 if k == "d0,d9,p10" else 1)
         nbytes = S * (10 + e) * L if k != "encode" else S * 14 * L
         ms = float(np.median(v))
-        print(json.dumps({"pattern": k, "decode_kernel": d, "lib": os.path.basename(H.LIB_PATH), "ms_med": round(ms, 3),
+        print(json.dumps({"pattern": k, "vec_per_thread": d, "lib": os.path.basename(H.LIB_PATH), "ms_med": round(ms, 3),
                           "GB_s": round(nbytes / ms / 1e6, 1)}), flush=True)
 
 

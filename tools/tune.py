@@ -30,8 +30,6 @@ def main():
     ap.add_argument("--rots", default="0", help="hashed per-stripe chunk rotation (0/1)")
     ap.add_argument("--wgs", default="256", help="RS(10,4) workgroup sizes (256/512/1024)")
     ap.add_argument("--encs", default="0", help="encode kernel: 0 table lookup, 1 bit-sliced")
-    ap.add_argument("--decs", default="1", help="decode kernel: 0 table, 1 bit-sliced (zero page), 2 bit-sliced "
-                                                "(branches)")
     ap.add_argument("--pad", type=int, default=0, help="extra bytes between shards (breaks 2^20 strides)")
     ap.add_argument("--tile", type=int, default=0,
                     help="interleaved layout: every shard split in tiles of this many bytes, the 14 "
@@ -57,14 +55,13 @@ def main():
     ints = lambda x: [int(y) for y in x.split(",")]
     configs = list(itertools.product(ints(args.modes), ints(args.vecs), ints(args.blocks), ints(args.remaps),
                                      ints(args.bpcs), ints(args.parts), ints(args.rots), ints(args.wgs),
-                                     ints(args.encs), ints(args.decs)))
+                                     ints(args.encs)))
     res = {c: {"enc": [], "dec": []} for c in configs}
     s = torch.cuda.current_stream()
     for _ in range(args.rounds):
         for c in configs:
-            mode, v, b, rm, bpc, parts, rot, wg, enc, dec = c
+            mode, v, b, rm, bpc, parts, rot, wg, enc = c
             H.lib.hec_set_encode_kernel(enc)
-            H.lib.hec_set_decode_kernel(dec)
             H.lib.hec_set_kernel_mode(mode)
             H.lib.hec_set_workgroup_size(wg)
             H.lib.hec_set_xcd_parts(parts)
@@ -81,7 +78,6 @@ def main():
             res[c]["dec"].append(e1.elapsed_time(e2))
     H.lib.hec_set_kernel_mode(0)
     H.lib.hec_set_encode_kernel(1)
-    H.lib.hec_set_decode_kernel(1)
     H.lib.hec_set_xcd_parts(1)
     H.lib.hec_set_chunk_rotation(0)
     H.lib.hec_set_workgroup_size(256)
@@ -92,7 +88,6 @@ def main():
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "pad": args.pad, "tile": args.tile,
                           "mode": ["gf", "xor_ceiling"][c[0]], "vec_per_thread": c[1], "max_blocks": c[2],
                           "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7], "encode_kernel": ["table", "bitslice"][c[8]],
-                          "decode_kernel": ["table", "bitslice_zp", "bitslice_branch"][c[9]],
                           "enc_ms_med": round(float(np.median(enc)), 3), "enc_ms_min": round(float(enc.min()), 3),
                           "enc_GBps": round(nbytes / np.median(enc) / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 3),

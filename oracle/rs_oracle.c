@@ -18,7 +18,9 @@
  * Loop order follows upstream code_some_slices: input-major, each output
  * slice mul (first input) or mul-xor (later inputs) over the whole slice.
  *
- * Pinned by tests/golden/upstream_kat.json and cross-checked against
+ * PARITY UNPINNED by the reference (it holds no EC tests or vectors and
+ * cannot be built here). Checked against the upstream crate's published KATs
+ * (tests/golden/upstream_kat.json) and cross-checked against
  * oracle/rs_oracle.py on the fixtures under tests/golden/.
  */
 #include <stdint.h>

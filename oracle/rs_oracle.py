@@ -24,9 +24,13 @@ feature ``simd-accel`` -- /root/reference/Cargo.toml:72,
 * File layout -- /root/reference/helyim-ec/src/encoder.rs:39-307 (restated in
   ``write_ec_files`` / ``rebuild_ec_files`` below, line cites inline).
 
-Parity pinning: helyim has no EC tests. The oracle is pinned by
-the upstream crate's published known-answer tests (tests/golden/upstream_kat.json)
-and cross-checked against the independent C restatement in oracle/rs_oracle.c.
+PARITY UNPINNED (by the reference): helyim has no EC tests, fixtures or golden
+vectors, the arithmetic crate is not in /root/reference and Rust
+cannot be built here, so nothing the reference itself produced pins this
+oracle. What it is checked against instead: the upstream crate's published
+known-answer tests (mul/exp/inverse KATs and the RS(5,5) one-encode vector,
+committed as data in tests/golden/upstream_kat.json) and the independent C
+restatement in oracle/rs_oracle.c.
 """
 from __future__ import annotations
 

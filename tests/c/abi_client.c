@@ -22,6 +22,7 @@
 void* orc_rs_new(int k, int m);
 void orc_rs_free(void* p);
 void orc_encode(void* p, uint8_t* const* shards, size_t len, int simd);
+int orc_reconstruct(void* p, uint8_t* const* shards, const uint8_t* present, size_t len, int data_only, int simd);
 void orc_splitmix64_fill(uint64_t seed, uint8_t* out, size_t nbytes);
 int orc_write_ec_files(const char* base, uint64_t buf_size, uint64_t large, uint64_t small, int simd);
 
@@ -185,6 +186,61 @@ static void check_batch(hec_rs_t* rs, void* ors) {
     }
 }
 
+/* The call shape INTEGRATION.md §3 gives the degraded read
+ * (helyim-store/src/erasure_coding/mod.rs:403-491): one needle read spans
+ * several intervals, each on a shard that is gone; the reader fans in the
+ * other shards' same ranges (a shard whose remote read fails stays None,
+ * mod.rs:461-474) and, instead of one ReedSolomon::reconstruct per interval
+ * (mod.rs:426), makes ONE hec_rs_reconstruct_batch over all of the needle's
+ * intervals, then copies each interval's recovered shard out (mod.rs:486-488).
+ * Checked against the C oracle's per-interval reconstruct. */
+static void check_degraded_read_shape(hec_rs_t* rs, void* ors) {
+    enum { NI = 5 };
+    const size_t ilen[NI] = {1, 4096, 65536 + 3, 512, 1u << 20};
+    const int lost[NI] = {3, 0, 9, 12, 5};      /* shard_id_to_recover */
+    const int unavailable[NI] = {-1, 13, -1, 1, 10}; /* a survivor whose remote read failed */
+    uint8_t* bufs[NI * N];
+    size_t lens[NI * N];
+    uint8_t present[NI * N];
+    uint8_t* want[NI];
+    for (int j = 0; j < NI; ++j) {
+        uint8_t** full = alloc_stripe(ilen[j]);
+        for (int i = 0; i < K; ++i) orc_splitmix64_fill(7000 + 19 * j + i, full[i], ilen[j]);
+        orc_encode(ors, full, ilen[j], 0);
+        want[j] = malloc(ilen[j]);
+        memcpy(want[j], full[lost[j]], ilen[j]);
+        for (int i = 0; i < N; ++i) {
+            const int p = i != lost[j] && i != unavailable[j];
+            present[j * N + i] = (uint8_t)p;
+            lens[j * N + i] = p ? ilen[j] : 0;
+            bufs[j * N + i] = calloc(1, ilen[j]);  /* upstream: vec![0; len] for None slots */
+            if (p) memcpy(bufs[j * N + i], full[i], ilen[j]);
+        }
+        free_stripe(full);
+    }
+    size_t bad = 0;
+    CHECK(hec_rs_reconstruct_batch(rs, bufs, lens, present, NI, 0, &bad) == HEC_OK, "degraded-read batch");
+    for (int j = 0; j < NI; ++j) {
+        /* buf.copy_from_slice(data[shard_id_to_recover]) */
+        CHECK(memcmp(bufs[j * N + lost[j]], want[j], ilen[j]) == 0, "interval %d shard %d", j, lost[j]);
+        /* and the same bytes as the oracle's per-interval reconstruct */
+        uint8_t* o[N];
+        uint8_t op[N];
+        for (int i = 0; i < N; ++i) {
+            o[i] = calloc(1, ilen[j]);
+            op[i] = present[j * N + i];
+            if (op[i]) memcpy(o[i], bufs[j * N + i], ilen[j]);
+        }
+        CHECK(orc_reconstruct(ors, o, op, ilen[j], 0, 0) == 0, "oracle reconstruct %d", j);
+        for (int i = 0; i < N; ++i) {
+            CHECK(memcmp(o[i], bufs[j * N + i], ilen[j]) == 0, "interval %d shard %d vs oracle", j, i);
+            free(o[i]);
+        }
+        free(want[j]);
+        for (int i = 0; i < N; ++i) free(bufs[j * N + i]);
+    }
+}
+
 static int read_file(const char* path, uint8_t** out, size_t* n) {
     FILE* f = fopen(path, "rb");
     if (!f) return -1;
@@ -261,6 +317,7 @@ int main(int argc, char** argv) {
     const size_t lens[] = {1, 17, 4096, 65536 + 7};
     for (size_t j = 0; j < sizeof lens / sizeof lens[0]; ++j) check_encode_reconstruct(rs, ors, lens[j], 100 * j);
     check_batch(rs, ors);
+    check_degraded_read_shape(rs, ors);
     check_files(argv[2]);
     orc_rs_free(ors);
     hec_rs_free(rs);

@@ -1,0 +1,233 @@
+//! The surface helyim-ec uses, on libhec: `ReedSolomon::{new, encode, verify,
+//! reconstruct, reconstruct_data}` (reed_solomon_erasure 6.0.0, used at
+//! /root/reference/helyim-ec/src/encoder.rs:191,208-209,249-250,288 and
+//! helyim-store/src/erasure_coding/mod.rs:411-412,426), the batched degraded
+//! read, and `write_ec_files` / `rebuild_ec_files`
+//! (helyim-ec/src/encoder.rs:39-50). Swapping
+//! `use reed_solomon_erasure::{ReedSolomon, galois_8::Field}` for
+//! `use helyim_ec_hip::ReedSolomon` is the whole change at each call site.
+//!
+//! `Error` has upstream's variants in upstream's order, so the codes map 1:1;
+//! inside helyim a maintainer would `pub use reed_solomon_erasure::Error` and
+//! keep `to_err`'s table.
+
+use std::ffi::{CStr, CString};
+use std::os::raw::c_int;
+
+use hec_sys as sys;
+
+/// reed_solomon_erasure::Error, declaration order (codes 1..=13).
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum Error {
+    TooFewShards,
+    TooManyShards,
+    TooFewDataShards,
+    TooManyDataShards,
+    TooFewParityShards,
+    TooManyParityShards,
+    TooFewBufferShards,
+    TooManyBufferShards,
+    IncorrectShardSize,
+    TooFewShardsPresent,
+    EmptyShard,
+    InvalidShardFlags,
+    InvalidIndex,
+    /// libhec device / argument failure (codes >= 64): no upstream variant.
+    Device(i32),
+}
+
+pub fn to_err(code: c_int) -> Error {
+    use Error::*;
+    const RS: [Error; 13] = [TooFewShards, TooManyShards, TooFewDataShards, TooManyDataShards,
+                             TooFewParityShards, TooManyParityShards, TooFewBufferShards,
+                             TooManyBufferShards, IncorrectShardSize, TooFewShardsPresent, EmptyShard,
+                             InvalidShardFlags, InvalidIndex];
+    if (1..=13).contains(&code) { RS[(code - 1) as usize] } else { Device(code) }
+}
+
+fn check(code: c_int) -> Result<(), Error> {
+    if code == sys::HEC_OK { Ok(()) } else { Err(to_err(code)) }
+}
+
+/// The text libhec gives for the last failure on this thread.
+pub fn last_error_detail() -> String {
+    unsafe { CStr::from_ptr(sys::hec_last_error_detail()) }.to_string_lossy().into_owned()
+}
+
+pub struct ReedSolomon(*mut sys::hec_rs_t);
+unsafe impl Send for ReedSolomon {}
+unsafe impl Sync for ReedSolomon {} // immutable after new; libhec's device state is mutex-guarded
+
+impl ReedSolomon {
+    pub fn new(data_shards: usize, parity_shards: usize) -> Result<Self, Error> {
+        let mut h = std::ptr::null_mut();
+        check(unsafe { sys::hec_rs_new(data_shards, parity_shards, &mut h) })?;
+        Ok(Self(h))
+    }
+
+    pub fn raw(&self) -> *const sys::hec_rs_t {
+        self.0
+    }
+
+    pub fn data_shard_count(&self) -> usize {
+        unsafe { sys::hec_rs_data_shard_count(self.0) }
+    }
+
+    pub fn parity_shard_count(&self) -> usize {
+        unsafe { sys::hec_rs_parity_shard_count(self.0) }
+    }
+
+    pub fn total_shard_count(&self) -> usize {
+        unsafe { sys::hec_rs_total_shard_count(self.0) }
+    }
+
+    /// Parity of shards[0..data] into shards[data..total], in place.
+    pub fn encode<T: AsMut<[u8]>>(&self, shards: &mut [T]) -> Result<(), Error> {
+        let lens: Vec<usize> = shards.iter_mut().map(|s| s.as_mut().len()).collect();
+        let ptrs: Vec<*mut u8> = shards.iter_mut().map(|s| s.as_mut().as_mut_ptr()).collect();
+        check(unsafe { sys::hec_rs_encode(self.0, ptrs.as_ptr(), lens.as_ptr(), ptrs.len()) })
+    }
+
+    pub fn verify<T: AsRef<[u8]>>(&self, shards: &[T]) -> Result<bool, Error> {
+        let lens: Vec<usize> = shards.iter().map(|s| s.as_ref().len()).collect();
+        let ptrs: Vec<*const u8> = shards.iter().map(|s| s.as_ref().as_ptr()).collect();
+        let mut ok = 0;
+        check(unsafe { sys::hec_rs_verify(self.0, ptrs.as_ptr(), lens.as_ptr(), ptrs.len(), &mut ok) })?;
+        Ok(ok == 1)
+    }
+
+    /// Upstream semantics: missing `None` slots are allocated `vec![0; len]`
+    /// and filled; on error the slots are left as they were.
+    pub fn reconstruct(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+        self.reconstruct_impl(shards, false)
+    }
+
+    /// As `reconstruct`, but missing parity slots stay `None`.
+    pub fn reconstruct_data(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+        self.reconstruct_impl(shards, true)
+    }
+
+    fn reconstruct_impl(&self, shards: &mut [Option<Vec<u8>>], data_only: bool) -> Result<(), Error> {
+        let present: Vec<u8> = shards.iter().map(|s| s.is_some() as u8).collect();
+        let lens: Vec<usize> = shards.iter().map(|s| s.as_ref().map_or(0, |v| v.len())).collect();
+        let len = lens.iter().copied().find(|&l| l > 0).unwrap_or(0);
+        let k = self.data_shard_count();
+        for s in shards.iter_mut().filter(|s| s.is_none()) {
+            *s = Some(vec![0u8; len]);
+        }
+        let ptrs: Vec<*mut u8> = shards.iter_mut().map(|s| s.as_mut().unwrap().as_mut_ptr()).collect();
+        let rc = unsafe {
+            if data_only {
+                sys::hec_rs_reconstruct_data(self.0, ptrs.as_ptr(), lens.as_ptr(), present.as_ptr(), ptrs.len())
+            } else {
+                sys::hec_rs_reconstruct(self.0, ptrs.as_ptr(), lens.as_ptr(), present.as_ptr(), ptrs.len())
+            }
+        };
+        for (i, (s, &p)) in shards.iter_mut().zip(&present).enumerate() {
+            if p == 0 && (rc != 0 || (data_only && i >= k)) {
+                *s = None; // untouched on error; reconstruct_data leaves parity absent
+            }
+        }
+        check(rc)
+    }
+
+    /// Many independent stripes (e.g. all lost intervals of a needle read,
+    /// erasure_coding/mod.rs:403-491) in ONE GPU round trip. Stripe j is
+    /// `stripes[j]`, each with upstream `reconstruct` semantics. On error
+    /// nothing is written and the error names the first failing stripe.
+    pub fn reconstruct_batch(&self, stripes: &mut [Vec<Option<Vec<u8>>>]) -> Result<(), (Error, usize)> {
+        let n = self.total_shard_count();
+        let mut ptrs = Vec::with_capacity(stripes.len() * n);
+        let mut lens = Vec::with_capacity(stripes.len() * n);
+        let mut present = Vec::with_capacity(stripes.len() * n);
+        for st in stripes.iter_mut() {
+            let len = st.iter().flatten().map(|b| b.len()).next().unwrap_or(0);
+            for b in st.iter_mut() {
+                present.push(b.is_some() as u8);
+                lens.push(b.as_ref().map_or(0, |v| v.len()));
+                ptrs.push(b.get_or_insert_with(|| vec![0u8; len]).as_mut_ptr());
+            }
+        }
+        let mut bad = 0usize;
+        let rc = unsafe {
+            sys::hec_rs_reconstruct_batch(self.0, ptrs.as_ptr(), lens.as_ptr(), present.as_ptr(), stripes.len(), 0,
+                                          &mut bad)
+        };
+        if rc != 0 {
+            let mut it = present.iter();
+            for st in stripes.iter_mut() {
+                for b in st.iter_mut() {
+                    if *it.next().unwrap() == 0 {
+                        *b = None;
+                    }
+                }
+            }
+            return Err((to_err(rc), bad));
+        }
+        Ok(())
+    }
+}
+
+impl Drop for ReedSolomon {
+    fn drop(&mut self) {
+        unsafe { sys::hec_rs_free(self.0) }
+    }
+}
+
+/// helyim_ec::EcShardError (helyim-ec/src/errors.rs:55-66), with libhec's
+/// device failures as their own variant.
+#[derive(Debug)]
+pub enum EcShardError {
+    Io(String),
+    ErasureCoding(Error),
+    Underflow(String),
+    UnexpectedEcShardSize(String),
+    UnexpectedBlockSize(String),
+    Device(i32, String),
+}
+
+fn file_err(code: c_int) -> EcShardError {
+    let d = last_error_detail();
+    match code {
+        sys::HEC_ERR_IO => EcShardError::Io(d),
+        sys::HEC_ERR_UNDERFLOW => EcShardError::Underflow(d),
+        sys::HEC_ERR_UNEXPECTED_EC_SHARD_SIZE => EcShardError::UnexpectedEcShardSize(d),
+        sys::HEC_ERR_UNEXPECTED_BLOCK_SIZE => EcShardError::UnexpectedBlockSize(d),
+        c if (1..=13).contains(&c) => EcShardError::ErasureCoding(to_err(c)),
+        c => EcShardError::Device(c, d),
+    }
+}
+
+fn cstr(s: &str) -> Result<CString, EcShardError> {
+    CString::new(s).map_err(|e| EcShardError::Io(e.to_string()))
+}
+
+/// helyim_ec::write_ec_files (encoder.rs:39-46): base.dat -> base.ec00..ec13.
+pub fn write_ec_files(base_filename: &str) -> Result<(), EcShardError> {
+    let c = cstr(base_filename)?;
+    match unsafe { sys::hec_write_ec_files(c.as_ptr()) } {
+        0 => Ok(()),
+        code => Err(file_err(code)),
+    }
+}
+
+/// helyim_ec::rebuild_ec_files (encoder.rs:48-50): the rebuilt shard ids.
+pub fn rebuild_ec_files(base_filename: &str) -> Result<Vec<u32>, EcShardError> {
+    let c = cstr(base_filename)?;
+    let mut ids = [0u32; 14];
+    let mut n = 0usize;
+    match unsafe { sys::hec_rebuild_ec_files(c.as_ptr(), ids.as_mut_ptr(), &mut n) } {
+        0 => Ok(ids[..n].to_vec()),
+        code => Err(file_err(code)),
+    }
+}
+
+/// Multi-GPU servers: whole volumes per GPU, chosen on the
+/// calling thread before the file-layer call.
+pub fn select_device_for_volume(volume_id: u32) -> Result<i32, Error> {
+    let mut n = 0;
+    check(unsafe { sys::hec_device_count(&mut n) })?;
+    let d = (volume_id % n.max(1) as u32) as i32;
+    check(unsafe { sys::hec_set_device(d) })?;
+    Ok(d)
+}

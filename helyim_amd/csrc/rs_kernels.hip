@@ -18,6 +18,7 @@
 //    data is vector traffic: coalesced 16 B/lane loads and stores (1 KiB per
 //    wave instruction), non-temporal since every byte is touched once.
 #include <algorithm>
+#include <type_traits>
 
 #include "rs_kernels.hpp"
 #include "bitslice.hpp"
@@ -78,6 +79,28 @@ __device__ __forceinline__ void store_full(uint8_t* p, u32x4 v, bool aligned) {
     } else {
         __builtin_memcpy(p, &v, 16);
     }
+}
+
+// Streamed access at (uniform shard base) + (lane offset): the base is moved
+// to the global address space before the offset is added, so a 32-bit offset
+// becomes the saddr form (SGPR base + VGPR offset) with no 64-bit VALU math.
+typedef const __attribute__((address_space(1))) uint8_t* gcu8p;
+typedef __attribute__((address_space(1))) uint8_t* gu8p;
+template <typename OffT>
+__device__ __forceinline__ u32x4 load_at(const uint8_t* base, OffT o) {
+#if HEC_NT_LOAD
+    return __builtin_nontemporal_load((gcu32x4p)((gcu8p)(base) + o));
+#else
+    return *(gcu32x4p)((gcu8p)(base) + o);
+#endif
+}
+template <typename OffT>
+__device__ __forceinline__ void store_at(uint8_t* base, OffT o, u32x4 v) {
+#if HEC_NT_STORE
+    __builtin_nontemporal_store(v, (gu32x4p)((gu8p)(base) + o));
+#else
+    *(gu32x4p)((gu8p)(base) + o) = v;
+#endif
 }
 
 __device__ __noinline__ u32x4 load_tail(const uint8_t* p, uint64_t avail) {
@@ -291,18 +314,62 @@ __device__ __forceinline__ uint32_t remap_block(uint32_t b, uint32_t nb, uint32_
     return (j / mode) * (8 * mode) + x * mode + (j % mode);
 }
 
+// Workgroup -> (stripe, chunk) of the RS(10,4) fast paths.
+// FAST: the shipped mapping (XCD eighths, or identity) from the launcher's
+// constants (map_q8 / map_r8, FastDiv of the chunks per stripe): a handful of
+// scalar ops from blockIdx, no division, so a workgroup reaches its stripe's
+// mask load (decode) or its first data load (encode) a few cycles after
+// launch. Before, remap_block's and the stripe's runtime divisions were
+// expanded into ~100 VALU instructions and three dependent kernel-argument
+// loads sat in front of the mask load.
+// !FAST: every measurement mapping (runs of G chunks, regions per XCD,
+// hashed per-stripe rotation) through remap_block's divisions.
+template <bool FAST>
+__device__ __forceinline__ void fast_item(const ApplyArgs& a, uint32_t per_stripe, uint32_t& stripe,
+                                          uint32_t& chunk) {
+    const uint32_t b = blockIdx.x;
+    uint32_t item = b;
+    if constexpr (FAST) {
+        // Every kernel argument the workgroup will need, in SGPRs at entry:
+        // one round trip, instead of loads the compiler sinks behind the
+        // remap branch and the decode's mask checks (each a further trip).
+        asm volatile("" ::"s"(a.in_base), "s"(a.in_stripe), "s"(a.in_shard), "s"(a.out_base), "s"(a.out_stripe),
+                     "s"(a.out_shard), "s"(a.len), "s"(a.masks), "s"(a.lut), "s"(a.tabs), "s"(a.xcd_remap),
+                     "s"(a.map_q8), "s"(a.map_r8), "s"(a.cps_mul), "s"(a.cps_shift), "s"(a.chunks_per_stripe));
+        if (a.xcd_remap) {  // XCD x = b % 8 takes the x-th eighth: x*q + min(x, r) + b/8
+            const uint32_t x = b & 7u, q = a.map_q8, r = a.map_r8;
+            item = x * q + (x < r ? x : r) + (b >> 3);
+        }
+        stripe = fastdiv(item, a.cps_mul, a.cps_shift);
+        chunk = item - stripe * per_stripe;
+    } else {
+        item = remap_block(b, gridDim.x, a.xcd_remap, a.xcd_parts);
+        stripe = item / per_stripe;
+        chunk = item - stripe * per_stripe;
+        if (a.chunk_rot) {  // per-stripe hashed rotation of the chunk order (bijective per stripe)
+            chunk += (stripe * 0x9E3779B1u) >> 8;
+            chunk %= per_stripe;
+        }
+    }
+}
+
 // One 4 KiB chunk of one RS(10,4) stripe. Encode (DEC=false): inputs 0..9 at
 // in_b, outputs 0..3 at out_b. Decode (DEC=true): in place at in_b == out_b,
 // shard ids from the present mask, tables at lut[mask] * 200 words.
-template <bool DEC, bool XORONLY, bool COMPACT = false, int TB = kThreads>
+// OffT: type of the lane's byte offset in the shard. uint32_t (every ragged
+// stripe, and strided batches of shards below 4 GiB) lets each load address
+// be a scalar shard base plus a 32-bit lane offset (global_load saddr form:
+// no per-load 64-bit VALU address math).
+template <bool DEC, bool XORONLY, bool COMPACT = false, int TB = kThreads, typename OffT = uint64_t>
 __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
                                             uint64_t out_shard, uint64_t len, uint32_t chunk, uint32_t mask_in,
                                             cu32p tab, cu32p lut, uint32_t* bad_count) {
     constexpr int K = 10, N = 14, R = 4;
     uint32_t in_id[K], out_id[R];
     uint32_t nout = R;
+    uint32_t mask = 0, plan = 0;
     if constexpr (DEC) {
-        const uint32_t mask = mask_in & ((1u << N) - 1);
+        mask = mask_in & ((1u << N) - 1);
         const uint32_t present = __builtin_popcount(mask);
         if (present < K) {
             if (chunk == 0 && threadIdx.x == 0 && bad_count) atomicAdd(bad_count, 1u);
@@ -322,14 +389,16 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
             out_id[r] = COMPACT ? r : (e ? __builtin_ctz(e) : 0);
             e &= e - 1;
         }
-        tab += lut[mask] * (K * R * 5);
+        // plan lookup issued now; its value is first needed after the data
+        // loads, so the scalar round trip overlaps them
+        plan = lut[mask];
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) in_id[i] = i;
 #pragma unroll
         for (int r = 0; r < R; ++r) out_id[r] = r;
     }
-    const uint64_t o = uint64_t(chunk) * (TB * kVecBytes) + threadIdx.x * kVecBytes;
+    const OffT o = OffT(chunk) * OffT(TB * kVecBytes) + OffT(threadIdx.x * kVecBytes);
     if (o >= len) return;
     const uint64_t avail = len - o;
     u32x4 acc[R];
@@ -338,13 +407,19 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
     if (avail >= kVecBytes) {
         u32x4 d[K];
 #pragma unroll
-        for (int i = 0; i < K; ++i) d[i] = load_full(in_b + uint64_t(in_id[i]) * in_shard + o, true);
+        for (int i = 0; i < K; ++i) d[i] = load_at(in_b + uint64_t(in_id[i]) * in_shard, o);
 #if HEC_LOADS_FIRST
         // all ten loads in flight before any math: without this fence the
         // scheduler interleaves them with the table multiply two at a time
         // (36 VGPRs, but one wave then waits on HBM five times per chunk)
         __builtin_amdgcn_sched_barrier(0);
 #endif
+        // opaque here: the table address math (and so the wait for the plan
+        // lookup) cannot be hoisted above the data loads
+        if constexpr (DEC) {
+            asm volatile("" : "+s"(plan));
+            tab += plan * (K * R * 5);
+        }
         if constexpr (XORONLY) {
 #pragma unroll
             for (int i = 0; i < K; ++i) mac<R, true>(acc, d[i], tab + i * (R * 5));
@@ -359,8 +434,12 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
         for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if (r < int(nout)) store_full(out_b + uint64_t(out_id[r]) * out_shard + o, acc[r], true);
+            if (r < int(nout)) store_at(out_b + uint64_t(out_id[r]) * out_shard, o, acc[r]);
     } else {
+        if constexpr (DEC) {
+            asm volatile("" : "+s"(plan));
+            tab += plan * (K * R * 5);
+        }
         for (int i = 0; i < K; ++i) {
             const u32x4 d = load_tail(in_b + uint64_t(in_id[i]) * in_shard + o, avail);
             gf_mac<R>(acc, d, tab + i * (R * 5));
@@ -370,37 +449,33 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
     }
 }
 
-template <bool DEC, bool XORONLY, int TB>
+// FAST: the shipped mapping at 256 threads with shards below 4 GiB (see
+// fast_item); otherwise the measurement mappings and 64-bit lane offsets.
+template <bool DEC, bool XORONLY, int TB, bool FAST>
 __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
-    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
-    const uint32_t stripe = item / a.chunks_per_stripe;
-    uint32_t chunk = item - stripe * a.chunks_per_stripe;
-    if (a.chunk_rot) {  // per-stripe hashed rotation of the chunk order (bijective per stripe)
-        chunk += (stripe * 0x9E3779B1u) >> 8;
-        chunk %= a.chunks_per_stripe;
-    }
+    uint32_t stripe, chunk;
+    fast_item<FAST>(a, a.chunks_per_stripe, stripe, chunk);
     const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
-    rs104_chunk<DEC, XORONLY, false, TB>(a.in_base + uint64_t(stripe) * a.in_stripe,
-                                         a.out_base + uint64_t(stripe) * a.out_stripe,
-                              a.in_shard, a.out_shard, a.len, chunk, mask, as_const(a.tabs), as_const(a.lut),
-                              a.bad_count);
+    using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
+    rs104_chunk<DEC, XORONLY, false, TB, OffT>(a.in_base + uint64_t(stripe) * a.in_stripe,
+                                               a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard,
+                                               a.out_shard, a.len, chunk, mask, as_const(a.tabs), as_const(a.lut),
+                                               a.bad_count);
 }
 
 // Two 4 KiB chunks per workgroup (launch config vec_per_thread = 2; shard
 // length a multiple of 8 KiB): each lane issues the 20 loads of both chunks,
 // then does the math of the first while the second's loads are in flight.
 // Chunks 2p and 2p+1 share a stripe, hence shard ids and tables.
-template <bool DEC, bool XORONLY>
+template <bool DEC, bool XORONLY, bool FAST>
 __global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
     constexpr int K = 10, N = 14, R = 4, U = 2;
-    const uint32_t pair = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
-    const uint32_t pairs_per_stripe = a.chunks_per_stripe / U;
-    const uint32_t stripe = pair / pairs_per_stripe;
-    const uint32_t p = pair - stripe * pairs_per_stripe;
+    uint32_t stripe, p;
+    fast_item<FAST>(a, a.chunks_per_stripe / U, stripe, p);
     const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
     uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
     uint32_t in_id[K], out_id[R];
-    uint32_t nout = R;
+    uint32_t nout = R, plan = 0;
     cu32p tab = as_const(a.tabs);
     if constexpr (DEC) {
         const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
@@ -423,20 +498,26 @@ __global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
             out_id[r] = e ? __builtin_ctz(e) : 0;
             e &= e - 1;
         }
-        tab += as_const(a.lut)[mask] * (K * R * 5);
+        plan = as_const(a.lut)[mask];  // first used after the data loads
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) in_id[i] = i;
 #pragma unroll
         for (int r = 0; r < R; ++r) out_id[r] = r;
     }
-    const uint64_t o0 = uint64_t(p) * (U * kThreads * kVecBytes) + threadIdx.x * kVecBytes;
+    using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
+    const OffT o0 = OffT(p) * OffT(U * kThreads * kVecBytes) + OffT(threadIdx.x * kVecBytes);
     u32x4 d[U][K];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            d[u][i] = load_full(in_b + uint64_t(in_id[i]) * a.in_shard + o0 + u * (kThreads * kVecBytes), true);
+            d[u][i] = load_at(in_b + uint64_t(in_id[i]) * a.in_shard, o0 + OffT(u * (kThreads * kVecBytes)));
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (DEC) {
+        asm volatile("" : "+s"(plan));
+        tab += plan * (K * R * 5);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         // Opaque per chunk: the table words are re-read (scalar cache hits)
@@ -455,8 +536,7 @@ __global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (r < int(nout))
-                store_full(out_b + uint64_t(out_id[r]) * a.out_shard + o0 + u * (kThreads * kVecBytes), acc[r],
-                           true);
+                store_at(out_b + uint64_t(out_id[r]) * a.out_shard, o0 + OffT(u * (kThreads * kVecBytes)), acc[r]);
     }
 }
 
@@ -472,17 +552,17 @@ __global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
 // ---------------------------------------------------------------------------
 // One 2*TB*16-byte column range (`chunk`) of one stripe: inputs 0..9 at in_b,
 // parity 0..3 at out_b.
-template <int TB>
+template <int TB, typename OffT = uint64_t>
 __device__ __forceinline__ void rs104_bs_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
                                                uint64_t out_shard, uint32_t chunk) {
     constexpr int K = 10, R = 4;
-    const uint64_t o0 = uint64_t(chunk) * (TB * 2 * kVecBytes) + threadIdx.x * kVecBytes;
-    const uint64_t o1 = o0 + TB * kVecBytes;
+    const OffT o0 = OffT(chunk) * OffT(TB * 2 * kVecBytes) + OffT(threadIdx.x * kVecBytes);
+    const OffT o1 = o0 + OffT(TB * kVecBytes);
     u32x4 d[K][2];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        d[i][0] = load_full(in_b + uint64_t(i) * in_shard + o0, true);
-        d[i][1] = load_full(in_b + uint64_t(i) * in_shard + o1, true);
+        d[i][0] = load_at(in_b + uint64_t(i) * in_shard, o0);
+        d[i][1] = load_at(in_b + uint64_t(i) * in_shard, o1);
     }
     uint32_t p[K * 8];
 #pragma unroll
@@ -499,20 +579,18 @@ __device__ __forceinline__ void rs104_bs_chunk(const uint8_t* in_b, uint8_t* out
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         transpose8(q + 8 * j);
-        store_full(out_b + uint64_t(j) * out_shard + o0, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]},
-                   true);
-        store_full(out_b + uint64_t(j) * out_shard + o1,
-                   u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]}, true);
+        store_at(out_b + uint64_t(j) * out_shard, o0, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]});
+        store_at(out_b + uint64_t(j) * out_shard, o1, u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]});
     }
 }
 
-template <int TB>
+template <int TB, bool FAST>
 __global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
-    const uint32_t item = remap_block(blockIdx.x, gridDim.x, a.xcd_remap, a.xcd_parts);
-    const uint32_t stripe = item / a.chunks_per_stripe;
-    const uint32_t chunk = item - stripe * a.chunks_per_stripe;
-    rs104_bs_chunk<TB>(a.in_base + uint64_t(stripe) * a.in_stripe, a.out_base + uint64_t(stripe) * a.out_stripe,
-                       a.in_shard, a.out_shard, chunk);
+    uint32_t stripe, chunk;
+    fast_item<FAST>(a, a.chunks_per_stripe, stripe, chunk);
+    using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
+    rs104_bs_chunk<TB, OffT>(a.in_base + uint64_t(stripe) * a.in_stripe,
+                             a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, chunk);
 }
 
 // Ragged encode with every stripe length a multiple of 8 KiB: workgroup ->
@@ -524,7 +602,7 @@ __global__ __launch_bounds__(kThreads) void rs104_bs_ragged_kernel(RaggedArgs a)
     const uint64_t off = it->off, stride = it->shard_stride;
     const uint32_t first = it->first_block;
     const uint8_t* b = a.base + off;
-    rs104_bs_chunk<kThreads>(b, a.base + off + 10 * stride, stride, stride, blk - first);
+    rs104_bs_chunk<kThreads, uint32_t>(b, a.base + off + 10 * stride, stride, stride, blk - first);
 }
 
 hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
@@ -539,6 +617,22 @@ hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
     return hipSuccess;
 }
 
+// Launch constants of fast_item: the XCD eighths of the grid and the chunks
+// per stripe as a multiply-shift divisor.
+static void set_fast_map(ApplyArgs& a, uint64_t n_blocks, uint32_t per_stripe) {
+    a.map_q8 = uint32_t(n_blocks / 8);
+    a.map_r8 = uint32_t(n_blocks % 8);
+    const FastDiv f = make_fastdiv(per_stripe);
+    a.cps_mul = f.mul;
+    a.cps_shift = f.shift;
+}
+// fast_item<true> covers the shipped mappings (XCD eighths or identity, one
+// region per XCD, no rotation) and 32-bit lane offsets (shards below 4 GiB).
+static bool fast_map_ok(const LaunchConfig& cfg, uint64_t len) {
+    return (cfg.xcd_remap == 0 || cfg.xcd_remap == 1) && cfg.xcd_parts <= 1 && cfg.chunk_rot == 0 &&
+           len <= 0xFFFFFFFFull;
+}
+
 template <int TB>
 static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
     const uint64_t chunk = uint64_t(TB) * 2 * kVecBytes;
@@ -547,8 +641,12 @@ static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
+    set_fast_map(a, a.n_items, a.chunks_per_stripe);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs104_bs_encode_kernel<TB>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
+    if (fast_map_ok(cfg, a.len))
+        hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, true>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
+    else
+        hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, false>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -574,8 +672,8 @@ __global__ __launch_bounds__(kThreads) void rs104_ragged_kernel(RaggedArgs a) {
     const uint32_t len = it->len, mask = it->mask, first = it->first_block;
     uint8_t* b = a.base + off;
     uint8_t* o = COMPACT ? a.base + it->out_off : (DEC ? b : b + 10 * stride);
-    rs104_chunk<DEC, false, COMPACT>(b, o, stride, stride, len, blk - first, mask, as_const(a.tabs),
-                                     as_const(a.lut), a.bad_count);
+    rs104_chunk<DEC, false, COMPACT, kThreads, uint32_t>(b, o, stride, stride, len, blk - first, mask,
+                                                         as_const(a.tabs), as_const(a.lut), a.bad_count);
 }
 
 hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream) {
@@ -604,8 +702,14 @@ static hipError_t launch_rs104_tb(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
     a.chunk_rot = uint32_t(cfg.chunk_rot);
+    set_fast_map(a, a.n_items, a.chunks_per_stripe);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY, TB>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
+    if (TB == kThreads && fast_map_ok(cfg, a.len))
+        hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY, kThreads, true>), dim3(uint32_t(a.n_items)), dim3(TB), lds,
+                           stream, a);
+    else
+        hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY, TB, false>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream,
+                           a);
     return hipGetLastError();
 }
 
@@ -619,9 +723,15 @@ static hipError_t launch_rs104_pair(ApplyArgs a, const LaunchConfig& cfg, hipStr
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
+    a.chunk_rot = 0;  // the pair kernel has no rotated order
+    set_fast_map(a, a.n_items / 2, a.chunks_per_stripe / 2);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs104_pair_kernel<DEC, XORONLY>), dim3(uint32_t(a.n_items / 2)), dim3(kThreads), lds, stream,
-                       a);
+    if (fast_map_ok(cfg, a.len))
+        hipLaunchKernelGGL((rs104_pair_kernel<DEC, XORONLY, true>), dim3(uint32_t(a.n_items / 2)), dim3(kThreads), lds,
+                           stream, a);
+    else
+        hipLaunchKernelGGL((rs104_pair_kernel<DEC, XORONLY, false>), dim3(uint32_t(a.n_items / 2)), dim3(kThreads),
+                           lds, stream, a);
     return hipGetLastError();
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "fastdiv.hpp"
+
 namespace hec {
 
 // One coding plan: nout output rows = coefficient matrix (nout x nin) applied
@@ -50,6 +52,10 @@ struct ApplyArgs {
     uint32_t chunk_rot;          // 1: rotate each stripe's chunk order by a hash of the stripe id
     uint32_t fast104;            // 1: RS(10,4) plan set with 4-row tables; encode = plan 0 at
                                  //    offset 0, decode = tables at lut[mask] * 200 words
+    // Launcher-computed workgroup -> chunk map of the RS(10,4) fast paths, so
+    // the kernels derive (stripe, chunk) in a few scalar ops with no division:
+    uint32_t map_q8, map_r8;     // workgroups / 8 and % 8 (XCD eighths remap)
+    uint32_t cps_mul, cps_shift; // item / chunks_per_stripe as a multiply-shift (FastDiv)
 };
 
 // Ragged RS(10,4) batch (every stripe its own length / stride / mask); all

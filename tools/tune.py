@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--wgs", default="256", help="RS(10,4) workgroup sizes (256/512/1024)")
     ap.add_argument("--encs", default="0", help="encode kernel: 0 table lookup, 1 bit-sliced")
     ap.add_argument("--pad", type=int, default=0, help="extra bytes between shards (breaks 2^20 strides)")
+    ap.add_argument("--stripe-pad", type=int, default=0, help="extra bytes between stripes (shards stay 1 MiB apart)")
     ap.add_argument("--tile", type=int, default=0,
                     help="interleaved layout: every shard split in tiles of this many bytes, the 14 "
                          "tiles of one column range stored together ([S*L/tile][14][tile])")
@@ -46,7 +47,10 @@ def main():
         S, L = S * rep, args.tile
         mask_np = np.repeat(mask_np, rep)
     rs = H.ReedSolomon(10, 4)
-    t = torch.empty((S, 14, L + args.pad), dtype=torch.uint8, device="cuda")[:, :, :L]
+    if args.stripe_pad:
+        t = torch.empty((S, 14 * L + args.stripe_pad), dtype=torch.uint8, device="cuda")[:, :14 * L].view(S, 14, L)
+    else:
+        t = torch.empty((S, 14, L + args.pad), dtype=torch.uint8, device="cuda")[:, :, :L]
     B.fill_splitmix(t, 10 * L, 0x5EED0000)
     masks = torch.from_numpy(mask_np).cuda()
     B.encode_batch(rs, t)
@@ -85,7 +89,8 @@ def main():
     nbytes = S * 14 * L
     for c in configs:
         enc, dec = np.array(res[c]["enc"]), np.array(res[c]["dec"])
-        print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "pad": args.pad, "tile": args.tile,
+        print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "pad": args.pad, "stripe_pad": args.stripe_pad,
+                          "tile": args.tile,
                           "mode": ["gf", "xor_ceiling"][c[0]], "vec_per_thread": c[1], "max_blocks": c[2],
                           "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7], "encode_kernel": ["table", "bitslice"][c[8]],
                           "enc_ms_med": round(float(np.median(enc)), 3), "enc_ms_min": round(float(enc.min()), 3),
@@ -96,7 +101,7 @@ def main():
     B.fill_splitmix(t, 10 * L, 0x5EED0000)
     B.encode_batch(rs, t)
     torch.cuda.synchronize()
-    if not args.pad:
+    if not args.pad and not args.stripe_pad:
         assert torch.equal(t[:8], good)
 
 

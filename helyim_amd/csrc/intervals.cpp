@@ -16,10 +16,38 @@
 namespace hec {
 namespace {
 
+// Metadata (RaggedItems + workgroup map) of one device-resident ragged call:
+// pinned staging and its device copy. The calls take slots round-robin, so a
+// call waits only for the kernel that used its slot kMetaSlots calls ago, not
+// for the previous call's kernel (a back-to-back encode / reconstruct stream
+// keeps the GPU fed while the host builds the next map).
+struct MetaSlot {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+    hipEvent_t free = nullptr;  // recorded after the kernel that read this slot
+    int reserve(size_t bytes) {
+        if (free) HEC_HIP(hipEventSynchronize(free));
+        else HEC_HIP(hipEventCreateWithFlags(&free, hipEventDisableTiming));
+        if (bytes <= cap) return HEC_OK;
+        if (h) HEC_HIP(hipHostFree(h));
+        if (d) HEC_HIP(hipFree(d));
+        h = d = nullptr;
+        cap = 0;
+        const size_t want = std::max(bytes, size_t(1) << 20);
+        HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&h), want));
+        HEC_HIP(hipMalloc(reinterpret_cast<void**>(&d), want));
+        cap = want;
+        return HEC_OK;
+    }
+};
+constexpr int kMetaSlots = 4;
+
 struct RaggedScratch {
     std::mutex mu;
     hipStream_t stream = nullptr;
-    hipEvent_t meta_free = nullptr;  // device-API calls: meta buffers reusable once this fires
+    MetaSlot slots[kMetaSlots];  // device-API ragged calls
+    unsigned next_slot = 0;
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
     size_t cap = 0;
@@ -247,14 +275,12 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     if (!rs || !d_base || (n && !descs)) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
     if (!(rs->k == 10 && rs->m == 4))
         return fail(HEC_ERR_INVALID_ARGUMENT, "ragged device batches are RS(10,4) only");
-    std::vector<RaggedItem> items;
-    std::vector<uint32_t> block_item;
-    items.reserve(n);
     // encode of lengths that are all multiples of 8 KiB: the bit-sliced kernel
     const LaunchConfig cfg = launch_config();
     bool bitslice = !decode && cfg.bitslice != 0 && cfg.mode == 0;
     for (uint32_t j = 0; j < n && bitslice; ++j) bitslice = descs[j].shard_len % kBsChunk == 0;
     const uint32_t chunk_bytes = bitslice ? kBsChunk : 4096;
+    uint64_t n_blocks = 0;
     for (uint32_t j = 0; j < n; ++j) {
         const hec_stripe_desc& d = descs[j];
         if (d.shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "stripe " + std::to_string(j));
@@ -263,35 +289,40 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
             return fail(HEC_ERR_INVALID_ARGUMENT, "stripe " + std::to_string(j) +
                                                       ": offset/stride must be 16-byte aligned, stride >= len");
         // 64-bit: a shard_len near 2^32 must not wrap to 0 or 1 chunks
-        const uint64_t chunks = (uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes;
-        if (block_item.size() + chunks > UINT32_MAX)
-            return fail(HEC_ERR_INVALID_ARGUMENT, "ragged batch above 2^32 workgroups");
-        items.push_back(RaggedItem{d.offset, d.shard_stride, d.shard_len, d.present_mask,
-                                   uint32_t(block_item.size()), 0, 0});
-        block_item.insert(block_item.end(), chunks, j);
+        n_blocks += (uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes;
+        if (n_blocks > UINT32_MAX) return fail(HEC_ERR_INVALID_ARGUMENT, "ragged batch above 2^32 workgroups");
     }
-    if (items.empty()) return HEC_OK;
+    if (n == 0) return HEC_OK;
     GeomDevice* gd;
     int rc = geom_device(rs, &gd);
     if (rc) return rc;
     RaggedScratch* sc;
     if ((rc = ragged_scratch(&sc))) return rc;
     std::lock_guard<std::mutex> lk(sc->mu);
-    const size_t items_bytes = items.size() * sizeof(RaggedItem);
+    const size_t items_bytes = size_t(n) * sizeof(RaggedItem);
     const size_t map_off = (items_bytes + 255) / 256 * 256;
-    const size_t meta = map_off + block_item.size() * 4;
-    if (sc->meta_free) HEC_HIP(hipEventSynchronize(sc->meta_free));  // previous call's kernel done
-    if ((rc = sc->reserve(0, meta))) return rc;
-    if (!sc->meta_free) HEC_HIP(hipEventCreateWithFlags(&sc->meta_free, hipEventDisableTiming));
+    const size_t meta = map_off + n_blocks * 4;
+    MetaSlot& slot = sc->slots[sc->next_slot++ % kMetaSlots];
+    if ((rc = slot.reserve(meta))) return rc;  // waits for this slot's previous kernel only
+    if (!sc->stream) HEC_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     if (decode && (rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
-    std::memcpy(sc->hmeta, items.data(), items_bytes);
-    std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
-    HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, stream));
+    // items and workgroup map written straight into the pinned slot
+    RaggedItem* items = reinterpret_cast<RaggedItem*>(slot.h);
+    uint32_t* block_item = reinterpret_cast<uint32_t*>(slot.h + map_off);
+    uint32_t first = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const hec_stripe_desc& d = descs[j];
+        const uint32_t chunks = uint32_t((uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes);
+        items[j] = RaggedItem{d.offset, d.shard_stride, d.shard_len, d.present_mask, first, 0, 0};
+        std::fill(block_item + first, block_item + first + chunks, j);
+        first += chunks;
+    }
+    HEC_HIP(hipMemcpyAsync(slot.d, slot.h, meta, hipMemcpyHostToDevice, stream));
     RaggedArgs ra{};
     ra.base = d_base;
-    ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
-    ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
-    ra.n_blocks = uint32_t(block_item.size());
+    ra.items = reinterpret_cast<const RaggedItem*>(slot.d);
+    ra.block_item = reinterpret_cast<const uint32_t*>(slot.d + map_off);
+    ra.n_blocks = uint32_t(n_blocks);
     ra.tabs = decode ? gd->decode_dense.tabs : gd->encode.tabs;
     ra.lut = decode ? gd->decode_dense.lut : nullptr;
     ra.bad_count = d_bad;
@@ -299,7 +330,7 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
         HEC_HIP(launch_rs104_bs_ragged(ra, stream));
     else
         HEC_HIP(launch_rs104_ragged(ra, decode, stream));
-    HEC_HIP(hipEventRecord(sc->meta_free, stream));
+    HEC_HIP(hipEventRecord(slot.free, stream));
     return HEC_OK;
 }
 

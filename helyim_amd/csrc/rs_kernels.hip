@@ -86,8 +86,22 @@ __device__ __forceinline__ void store_full(uint8_t* p, u32x4 v, bool aligned) {
 // becomes the saddr form (SGPR base + VGPR offset) with no 64-bit VALU math.
 typedef const __attribute__((address_space(1))) uint8_t* gcu8p;
 typedef __attribute__((address_space(1))) uint8_t* gu8p;
+// Measurement variants (Makefile VARIANTS): HEC_LOAD_CPOL / HEC_STORE_CPOL >= 0
+// route 32-bit-offset accesses through raw buffer instructions with that
+// cache-policy word (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
+#ifndef HEC_LOAD_CPOL
+#define HEC_LOAD_CPOL -1
+#endif
+#ifndef HEC_STORE_CPOL
+#define HEC_STORE_CPOL -1
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t shard_rsrc(const uint8_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, int(0xFFFFFFFFu), 0x00020000);
+}
 template <typename OffT>
 __device__ __forceinline__ u32x4 load_at(const uint8_t* base, OffT o) {
+    if constexpr (sizeof(OffT) == 4 && HEC_LOAD_CPOL >= 0)
+        return __builtin_amdgcn_raw_buffer_load_b128(shard_rsrc(base), o, 0, HEC_LOAD_CPOL);
 #if HEC_NT_LOAD
     return __builtin_nontemporal_load((gcu32x4p)((gcu8p)(base) + o));
 #else
@@ -96,6 +110,10 @@ __device__ __forceinline__ u32x4 load_at(const uint8_t* base, OffT o) {
 }
 template <typename OffT>
 __device__ __forceinline__ void store_at(uint8_t* base, OffT o, u32x4 v) {
+    if constexpr (sizeof(OffT) == 4 && HEC_STORE_CPOL >= 0) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, shard_rsrc(base), o, 0, HEC_STORE_CPOL);
+        return;
+    }
 #if HEC_NT_STORE
     __builtin_nontemporal_store(v, (gu32x4p)((gu8p)(base) + o));
 #else

@@ -1,0 +1,69 @@
+"""Device-resident mixed workload (BASELINE config 5, as bench.py's
+mixed_section): 512 stripes of 64 KiB..4 MiB shards, 0..4 erasures, one
+ragged encode + one ragged reconstruct per rep. Prints the data-payload
+GiB/s per round and the per-launch split (HIP events) so host gaps between
+launches show up: gap = wall per rep - encode - reconstruct. HEC_LIB_PATH
+selects a measurement build.
+
+python tools/mixed_probe.py [--rounds 5] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--stripes", type=int, default=512)
+    args = ap.parse_args()
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    import bench
+    rs = H.ReedSolomon(10, 4)
+    rng = np.random.default_rng(0x5E)
+    lens = [(64 << 10) << i for i in range(7)]
+    n = args.stripes
+    Ls = rng.choice(lens, n)
+    es = rng.integers(0, 5, n)
+    full = (1 << 14) - 1
+    masks = [full & ~int(sum(1 << int(i) for i in rng.choice(14, int(e), replace=False))) for e in es]
+    descs, off = [], 0
+    for s in range(n):
+        descs.append((off, int(Ls[s]), int(Ls[s]), int(masks[s])))
+        off += 14 * int(Ls[s])
+    dev = torch.empty(off, dtype=torch.uint8, device="cuda")
+    for s, (o, st, L, _) in enumerate(descs):
+        B.fill_splitmix(dev[o:o + 10 * L].view(1, 1, -1), 10 * L, bench.rank_seed_base(0) + s)
+    payload = sum(10 * d[2] for d in descs) + sum(10 * d[2] for d in descs if d[3] != full)
+    B.encode_ragged(rs, dev, descs)
+    B.reconstruct_ragged(rs, dev, descs)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    for r in range(args.rounds):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
+        ev[0].record(st)
+        for i in range(args.reps):
+            B.encode_ragged(rs, dev, descs)
+            ev[2 * i + 1].record(st)
+            B.reconstruct_ragged(rs, dev, descs)
+            ev[2 * i + 2].record(st)
+        torch.cuda.synchronize()
+        enc = np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)])
+        dec = np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)])
+        wall = ev[0].elapsed_time(ev[-1]) / args.reps
+        print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "round": r, "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
+                          "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3), "dec_ms": round(float(dec), 3),
+                          "payload_GiB": round(payload / 2**30, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -675,6 +675,50 @@ def test_ragged_shard_len_near_4gib(gpu):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("L", [(1 << 32) - 8192, (1 << 32) - 4096, (1 << 32) + 8192])
+def test_strided_batch_shard_len_near_4gib(gpu, L):
+    """Two-stripe strided device batches (112 GiB in HBM) at the edge of the
+    fast kernels' 32-bit lane offsets (fast_map_ok: shards below 4 GiB):
+    2^32 - 8 KiB runs the bit-sliced encode with SGPR shard bases + 32-bit
+    offsets, 2^32 - 4 KiB the table encode on the same fast map, 2^32 + 8 KiB
+    the 64-bit-offset kernels. Both stripes' parity and a per-stripe
+    4-erasure rebuild are checked against the C oracle on the first and last
+    64 KiB of every shard, where a wrapped offset would land."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, W = 2, 1 << 16
+    torch.cuda.empty_cache()
+    t = torch.empty((S, 14, L), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(t, 10 * L, 0x5EED5000)
+    t[:, 10:].zero_()
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+
+    def cols(s, lo):
+        return t[s, :, lo:lo + W].cpu().numpy()
+
+    ref = {}
+    for s in range(S):
+        for lo in (0, L - W):
+            c = cols(s, lo)
+            assert np.array_equal(c[10:], corc.encode_stripes(np.ascontiguousarray(c[None, :10]))[0]), (L, s, lo)
+            ref[s, lo] = c
+    drops = ((0, 3, 11, 13), (2, 5, 9, 10))
+    masks = torch.tensor([0x3FFF & ~sum(1 << i for i in d) for d in drops], dtype=torch.int32, device="cuda")
+    for s, d in enumerate(drops):
+        for i in d:
+            t[s, i].zero_()
+    B.reconstruct_batch(rs, t, masks)
+    torch.cuda.synchronize()
+    for s in range(S):
+        for lo in (0, L - W):
+            assert np.array_equal(cols(s, lo), ref[s, lo]), (L, s, lo)
+    del t
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (12, 4), (8, 8), (1, 1)])
 def test_device_batches_generic_geometry(gpu, k, m):
     """hec_gpu_encode_batch / hec_gpu_reconstruct_batch on geometries other

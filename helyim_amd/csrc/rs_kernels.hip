@@ -166,8 +166,11 @@ typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
 // Two inputs at once: the six lookups of a row are folded into the
 // accumulator by three 3-input XORs (v_bitop3) instead of four ops.
+// nrows (wave-uniform, <= R): rows at or past it skip their math (a decode
+// with e < 4 erasures; scalar branches, the tables keep their 4-row stride).
 template <int R>
-__device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R], const u32x4 d0, const u32x4 d1, cu32p tab0, cu32p tab1) {
+__device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R], const u32x4 d0, const u32x4 d1, cu32p tab0, cu32p tab1,
+                                        uint32_t nrows = R) {
     uint32_t s[2][3][4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -179,12 +182,26 @@ __device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R], const u32x4 d0, const u
         s[1][1][w] = (x1 >> 3) & 0x07070707u;
         s[1][2][w] = (x1 >> 6) & 0x03030303u;
     }
+    // both inputs' table words for every row, requested before the row
+    // branches (the empty asm keeps the loads from sinking into them, where
+    // each row would wait on its own scalar round trip)
+    uint32_t ta[R * 5], tbw[R * 5];
+#pragma unroll
+    for (int j = 0; j < R * 5; ++j) {
+        ta[j] = tab0[j];
+        tbw[j] = tab1[j];
+    }
+    if (R < 4 || nrows < uint32_t(R)) {
+#pragma unroll
+        for (int j = 0; j < R * 5; ++j) asm volatile("" ::"s"(ta[j]), "s"(tbw[j]));
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const uint32_t a0l = tab0[r * 5 + 0], a0h = tab0[r * 5 + 1], a1l = tab0[r * 5 + 2], a1h = tab0[r * 5 + 3],
-                       a2 = tab0[r * 5 + 4];
-        const uint32_t b0l = tab1[r * 5 + 0], b0h = tab1[r * 5 + 1], b1l = tab1[r * 5 + 2], b1h = tab1[r * 5 + 3],
-                       b2 = tab1[r * 5 + 4];
+        if (r > 0 && uint32_t(r) >= nrows) break;
+        const uint32_t a0l = ta[r * 5 + 0], a0h = ta[r * 5 + 1], a1l = ta[r * 5 + 2], a1h = ta[r * 5 + 3],
+                       a2 = ta[r * 5 + 4];
+        const uint32_t b0l = tbw[r * 5 + 0], b0h = tbw[r * 5 + 1], b1l = tbw[r * 5 + 2], b1h = tbw[r * 5 + 3],
+                       b2 = tbw[r * 5 + 4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             const uint32_t p0 = __builtin_amdgcn_perm(a0h, a0l, s[0][0][w]);
@@ -443,7 +460,8 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
             for (int i = 0; i < K; ++i) mac<R, true>(acc, d[i], tab + i * (R * 5));
         } else {
 #pragma unroll
-            for (int i = 0; i < K; i += 2) gf_mac2<R>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5));
+            for (int i = 0; i < K; i += 2)
+                gf_mac2<R>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
         }
         // Materialise every row before the uniform `r < nout` store branches:
         // otherwise the compiler sinks each row's math into its branch, keeps

@@ -43,6 +43,10 @@ def main():
     pats = {"random4": bench.erasure_masks(S, 0), "p10-13": fixed((10, 11, 12, 13)),
             "d0-3": fixed((0, 1, 2, 3)), "d6-9": fixed((6, 7, 8, 9)), "0,5,10,13": fixed((0, 5, 10, 13)),
             "d0,d9,p10": fixed((0, 9, 10)), "one_d4": fixed((4,))}
+    rng = np.random.default_rng(0xE4)
+    for e in (1, 2, 3):  # per-stripe random patterns with exactly e erasures
+        pats[f"random{e}"] = np.array([full & ~int(sum(1 << int(i) for i in rng.choice(14, e, replace=False)))
+                                       for _ in range(S)], np.int32)
     masks = {k: torch.from_numpy(v).cuda() for k, v in pats.items()}
     decs = [int(x) for x in args.vecs.split(",")]
     res = {}
@@ -64,7 +68,7 @@ def main():
                 res.setdefault((k, d), []).append(e0.elapsed_time(e1))
     B.set_launch_config()
     for (k, d), v in res.items():
-        e = 4 if k in ("random4", "p10-13", "d0-3", "d6-9", "0,5,10,13") else (3 if k == "d0,d9,p10" else 1)
+        e = {"d0,d9,p10": 3, "one_d4": 1, "random1": 1, "random2": 2, "random3": 3}.get(k, 4)
         nbytes = S * (10 + e) * L if k != "encode" else S * 14 * L
         ms = float(np.median(v))
         print(json.dumps({"pattern": k, "vec_per_thread": d, "lib": os.path.basename(H.LIB_PATH), "ms_med": round(ms, 3),

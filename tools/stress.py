@@ -7,6 +7,7 @@ Worker threads run, for --seconds, a random mix of:
   * the batched ragged reconstruct (hec_rs_reconstruct_batch),
   * file-level write_ec_files / rebuild_ec_files on small volumes,
   * device batches on a private torch stream,
+  * device-resident ragged encode + reconstruct on a private stream,
 every result checked bit-exact against the C oracle. Prints one JSON line.
 Measurement / test tool only.
 
@@ -123,11 +124,44 @@ def main():
         assert np.array_equal(par, corc.encode_stripes(host)), "device"
         note("device_batch")
 
+    def device_ragged(rng, stream):
+        # device-resident ragged encode + reconstruct on a private stream (the
+        # metadata slots are shared by every thread of the device)
+        n = int(rng.integers(1, 24))
+        lens = [int(rng.choice([16, 4096 + 16 * int(rng.integers(0, 64)), 8192, 3 * 8192])) for _ in range(n)]
+        full = (1 << 14) - 1
+        descs, off = [], 0
+        for L in lens:
+            drop = rng.choice(14, int(rng.integers(0, 5)), replace=False)
+            descs.append((off, L, L, full & ~int(sum(1 << int(i) for i in drop))))
+            off += 14 * L
+        host = np.zeros(off, np.uint8)
+        for (o, _, L, _) in descs:
+            host[o:o + 10 * L] = rng.integers(0, 256, 10 * L, dtype=np.uint8)
+        with torch.cuda.stream(stream):
+            t = torch.from_numpy(host).cuda()
+            B.encode_ragged(rs, t, descs, stream=stream)
+            stream.synchronize()
+            enc = t.cpu().numpy()
+            for (o, _, L, m) in descs:
+                for i in range(14):
+                    if not (m >> i) & 1:
+                        t[o + i * L:o + (i + 1) * L] = 0
+            B.reconstruct_ragged(rs, t, descs, stream=stream)
+            stream.synchronize()
+            dec = t.cpu().numpy()
+        for (o, _, L, _) in descs:
+            want = corc.encode_stripes(np.ascontiguousarray(enc[o:o + 10 * L].reshape(1, 10, L)))[0]
+            assert np.array_equal(enc[o + 10 * L:o + 14 * L].reshape(4, L), want), "device_ragged encode"
+        assert np.array_equal(dec, enc), "device_ragged reconstruct"
+        note("device_ragged")
+
     def worker(t_id):
         rng = np.random.default_rng(1000 + t_id)
         torch.cuda.set_device(0)
         stream = torch.cuda.Stream()
-        ops = [percall, host_batch, ragged, lambda r: files(r, t_id), lambda r: device(r, stream)]
+        ops = [percall, host_batch, ragged, lambda r: files(r, t_id), lambda r: device(r, stream),
+               lambda r: device_ragged(r, stream)]
         while time.monotonic() < stop:
             op = ops[int(rng.integers(0, len(ops)))]
             try:

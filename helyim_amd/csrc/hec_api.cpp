@@ -5,6 +5,7 @@
 // kernels in rs_kernels.hip; there is no CPU fallback.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -333,8 +334,9 @@ int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
 int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uint64_t in_stripe,
               uint64_t in_shard, uint8_t* out_base, uint64_t out_stripe, uint64_t out_shard,
               uint64_t len, uint32_t n_stripes, const uint32_t* masks, uint32_t* bad,
-              hipStream_t s) {
+              hipStream_t s, Completion* done) {
     ApplyArgs a{};
+    if (done) HEC_TRY(done->arm(s, &a.done_count, &a.done_flag, &a.done_seq));
     a.in_base = in_base;
     a.in_stripe = in_stripe;
     a.in_shard = in_shard;
@@ -406,6 +408,41 @@ std::atomic<uint64_t>& host_staging_max() {
     return v;
 }
 
+std::atomic<uint64_t>& completion_flag_max() {
+    static std::atomic<uint64_t> v{uint64_t(1) << 20};
+    return v;
+}
+
+int Completion::arm(hipStream_t s, uint32_t** count_out, uint32_t** flag_out, uint32_t* seq_out) {
+    if (!host) {
+        HEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), 64, hipHostMallocCoherent));
+        *host = 0;
+        HEC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dflag), host, 0));
+        HEC_HIP(hipMalloc(reinterpret_cast<void**>(&count), 64));
+        HEC_HIP(hipMemsetAsync(count, 0, 64, s));  // ordered before the first signalling launch
+    }
+    if (++seq == 0) seq = 1;  // 0 is the flag's initial value
+    *count_out = count;
+    *flag_out = dflag;
+    *seq_out = seq;
+    return HEC_OK;
+}
+
+int Completion::wait(hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    while (__atomic_load_n(host, __ATOMIC_ACQUIRE) != seq) {
+        if ((++spins & 255) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
+            HEC_HIP(hipStreamSynchronize(s));
+            if (__atomic_load_n(host, __ATOMIC_ACQUIRE) != seq)
+                return fail(HEC_ERR_HIP, "kernel finished without its completion signal");
+            return HEC_OK;
+        }
+    }
+    return HEC_OK;
+}
+
 int device_scratch(Scratch** out) {
     int dev;
     int rc = current_device(&dev);
@@ -457,9 +494,16 @@ static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* co
         uint8_t* hpar = sc->hbuf + size_t(rs->k) * Lp;
         uint8_t* zh = zero_copy_enabled() ? pinned_device_ptr(sc->hbuf) : nullptr;
         if (zh) {  // the kernel reads the packed shards and writes parity over PCIe
+            Completion* done = uint64_t(rs->k) * L <= completion_flag_max() ? &sc->done : nullptr;
             if ((rc = run_apply(gd->encode, uint32_t(rs->k), zh, 0, Lp, zh + size_t(rs->k) * Lp, 0, Lp,
-                                round_up(L, 16), 1, nullptr, nullptr, sc->stream)))
+                                round_up(L, 16), 1, nullptr, nullptr, sc->stream, done)))
                 return rc;
+            if (done) {
+                if ((rc = done->wait(sc->stream))) return rc;
+                parallel_for(size_t(rs->m), uint64_t(rs->m) * L,
+                             [&](size_t j) { std::memcpy(dst_of(int(j)), hpar + j * Lp, L); });
+                return HEC_OK;
+            }
         } else {
             HEC_HIP(hipMemcpyAsync(sc->dbuf, sc->hbuf, size_t(rs->k) * Lp, hipMemcpyHostToDevice, sc->stream));
             if ((rc = run_apply(gd->encode, uint32_t(rs->k), sc->dbuf, 0, Lp, par, 0, Lp, round_up(L, 16), 1,
@@ -644,6 +688,11 @@ int hec_set_encode_kernel(int kind) {
 
 int hec_set_host_staging(uint64_t max_bytes) {
     host_staging_max() = max_bytes;
+    return HEC_OK;
+}
+
+int hec_set_completion_signal(uint64_t max_bytes) {
+    completion_flag_max() = max_bytes;
     return HEC_OK;
 }
 

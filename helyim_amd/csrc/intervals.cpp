@@ -48,6 +48,7 @@ struct RaggedScratch {
     hipStream_t stream = nullptr;
     MetaSlot slots[kMetaSlots];  // device-API ragged calls
     unsigned next_slot = 0;
+    Completion done;             // small host calls (compact_reconstruct_104)
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
     size_t cap = 0;
@@ -160,27 +161,39 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     else
         parallel_for(jobs.size() * size_t(k), in_total, fill_one);
     if (first_err.load()) return first_err.load();
-    std::memcpy(sc->hmeta, items.data(), items_bytes);
-    const size_t map_off = (items_bytes + 255) / 256 * 256;
-    std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
-    HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, sc->stream));
     // zero-copy: the kernel reads the packed survivors and writes the rebuilt
     // shards in the pinned staging itself (no H2D / D2H of the payload)
     uint8_t* zh = zero_copy_enabled() ? pinned_device_ptr(sc->host) : nullptr;
     if (!zh) HEC_HIP(hipMemcpyAsync(sc->dev, sc->host, in_total, hipMemcpyHostToDevice, sc->stream));
     RaggedArgs ra{};
     ra.base = zh ? zh : sc->dev;
-    ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
-    ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
     ra.n_blocks = uint32_t(block_item.size());
     ra.tabs = gd->decode_dense.tabs;
     ra.lut = gd->decode_dense.lut;
     ra.compact = 1;
+    if (items.size() == 1) {  // one stripe (a per-call reconstruct): descriptor as a kernel argument
+        ra.inline_one = 1;
+        ra.one = items[0];
+    } else {
+        std::memcpy(sc->hmeta, items.data(), items_bytes);
+        const size_t map_off = (items_bytes + 255) / 256 * 256;
+        std::memcpy(sc->hmeta + map_off, block_item.data(), block_item.size() * 4);
+        HEC_HIP(hipMemcpyAsync(sc->dmeta, sc->hmeta, meta, hipMemcpyHostToDevice, sc->stream));
+        ra.items = reinterpret_cast<const RaggedItem*>(sc->dmeta);
+        ra.block_item = reinterpret_cast<const uint32_t*>(sc->dmeta + map_off);
+    }
+    // small zero-copy calls: completion from the kernel's own signal
+    const bool signal = zh && in_total <= completion_flag_max();
+    if (signal && (rc = sc->done.arm(sc->stream, &ra.done_count, &ra.done_flag, &ra.done_seq))) return rc;
     HEC_HIP(launch_rs104_ragged(ra, true, sc->stream));
     if (!zh)
         HEC_HIP(hipMemcpyAsync(sc->host + in_total, sc->dev + in_total, total - in_total, hipMemcpyDeviceToHost,
                                sc->stream));
-    HEC_HIP(hipStreamSynchronize(sc->stream));
+    if (signal) {
+        if ((rc = sc->done.wait(sc->stream))) return rc;
+    } else {
+        HEC_HIP(hipStreamSynchronize(sc->stream));
+    }
     // hand back the erased shards
     parallel_for(jobs.size(), total - in_total, [&](size_t j) {
         int r = 0;

@@ -273,6 +273,26 @@ __device__ __forceinline__ void apply_group(const ApplyArgs& a, const uint8_t* i
     }
 }
 
+// Completion signal of a launch for a host that spins on pinned memory
+// (small host calls): every wave drains its stores, the
+// workgroup meets at a barrier, lane 0 releases at system scope and counts
+// itself in; the last workgroup resets the counter and stores the sequence
+// number into the host flag. Every workgroup of the grid reaches this (the
+// kernels call it after their body, early exits included).
+__device__ __forceinline__ void signal_done(uint32_t* count, uint32_t* flag, uint32_t seq) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        const uint32_t blocks = gridDim.x * gridDim.y * gridDim.z;
+        if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == blocks - 1) {
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 template <int K, int U, bool ALIGNED, bool XORONLY = false>
 __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
     // XCD-aware chunk mapping: workgroups b, b+8, b+16, ... are dealt to one
@@ -315,6 +335,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
             }
         }
     }
+    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -497,6 +518,7 @@ __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
                                                a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard,
                                                a.out_shard, a.len, chunk, mask, as_const(a.tabs), as_const(a.lut),
                                                a.bad_count);
+    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
 // Two 4 KiB chunks per workgroup (launch config vec_per_thread = 2; shard
@@ -504,7 +526,7 @@ __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
 // then does the math of the first while the second's loads are in flight.
 // Chunks 2p and 2p+1 share a stripe, hence shard ids and tables.
 template <bool DEC, bool XORONLY, bool FAST>
-__global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
+__device__ __forceinline__ void rs104_pair_body(const ApplyArgs& a) {
     constexpr int K = 10, N = 14, R = 4, U = 2;
     uint32_t stripe, p;
     fast_item<FAST>(a, a.chunks_per_stripe / U, stripe, p);
@@ -576,6 +598,12 @@ __global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
     }
 }
 
+template <bool DEC, bool XORONLY, bool FAST>
+__global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
+    rs104_pair_body<DEC, XORONLY, FAST>(a);
+    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
+}
+
 // ---------------------------------------------------------------------------
 // Bit-sliced RS(10,4) encode (fixed parity matrix). A lane owns 32 bytes of
 // every shard (two 16-byte vectors TB*16 apart, so each load instruction stays
@@ -627,24 +655,34 @@ __global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
     using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
     rs104_bs_chunk<TB, OffT>(a.in_base + uint64_t(stripe) * a.in_stripe,
                              a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, chunk);
+    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
+}
+
+// Descriptor of the stripe workgroup blk works on: the kernel-argument copy
+// for a one-stripe launch, else the workgroup map and item table (scalar loads).
+__device__ __forceinline__ RaggedItem ragged_item(const RaggedArgs& a, uint32_t blk) {
+    if (a.inline_one) return a.one;
+    const __attribute__((address_space(4))) RaggedItem* p = as_const(a.items) + as_const(a.block_item)[blk];
+    return RaggedItem{p->off, p->shard_stride, p->len, p->mask, p->first_block, 0, p->out_off};
 }
 
 // Ragged encode with every stripe length a multiple of 8 KiB: workgroup ->
 // stripe map as rs104_ragged_kernel, one 8 KiB column range per workgroup.
 __global__ __launch_bounds__(kThreads) void rs104_bs_ragged_kernel(RaggedArgs a) {
     const uint32_t blk = blockIdx.x + a.block_base;
-    const uint32_t s = as_const(a.block_item)[blk];
-    const __attribute__((address_space(4))) RaggedItem* it = as_const(a.items) + s;
-    const uint64_t off = it->off, stride = it->shard_stride;
-    const uint32_t first = it->first_block;
+    const RaggedItem it = ragged_item(a, blk);
+    const uint64_t off = it.off, stride = it.shard_stride;
+    const uint32_t first = it.first_block;
     const uint8_t* b = a.base + off;
     rs104_bs_chunk<kThreads, uint32_t>(b, a.base + off + 10 * stride, stride, stride, blk - first);
+    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
 hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
     for (uint64_t b0 = 0; b0 < a.n_blocks; b0 += kMaxLaunchBlocks) {  // see kMaxLaunchBlocks
         RaggedArgs r = a;
         r.block_base = uint32_t(b0);
+        if (b0 + kMaxLaunchBlocks < a.n_blocks) r.done_flag = nullptr;  // the last launch signals
         const uint32_t nb = uint32_t(std::min<uint64_t>(kMaxLaunchBlocks, a.n_blocks - b0));
         hipLaunchKernelGGL(rs104_bs_ragged_kernel, dim3(nb), dim3(kThreads), 0, stream, r);
         hipError_t e = hipGetLastError();
@@ -702,20 +740,22 @@ static hipError_t launch_rs104_bs_cfg(const ApplyArgs& a, const LaunchConfig& cf
 template <bool DEC, bool COMPACT>
 __global__ __launch_bounds__(kThreads) void rs104_ragged_kernel(RaggedArgs a) {
     const uint32_t blk = blockIdx.x + a.block_base;
-    const uint32_t s = as_const(a.block_item)[blk];
-    const __attribute__((address_space(4))) RaggedItem* it = as_const(a.items) + s;
-    const uint64_t off = it->off, stride = it->shard_stride;
-    const uint32_t len = it->len, mask = it->mask, first = it->first_block;
-    uint8_t* b = a.base + off;
-    uint8_t* o = COMPACT ? a.base + it->out_off : (DEC ? b : b + 10 * stride);
-    rs104_chunk<DEC, false, COMPACT, kThreads, uint32_t>(b, o, stride, stride, len, blk - first, mask,
-                                                         as_const(a.tabs), as_const(a.lut), a.bad_count);
+    // one stripe (a per-call host reconstruct): its descriptor is a kernel
+    // argument, so the launch needs no metadata upload and no dependent loads
+    const RaggedItem it = ragged_item(a, blk);
+    uint8_t* b = a.base + it.off;
+    uint8_t* o = COMPACT ? a.base + it.out_off : (DEC ? b : b + 10 * it.shard_stride);
+    rs104_chunk<DEC, false, COMPACT, kThreads, uint32_t>(b, o, it.shard_stride, it.shard_stride, it.len,
+                                                         blk - it.first_block, it.mask, as_const(a.tabs),
+                                                         as_const(a.lut), a.bad_count);
+    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
 hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream) {
     for (uint64_t b0 = 0; b0 < a.n_blocks; b0 += kMaxLaunchBlocks) {  // see kMaxLaunchBlocks
         RaggedArgs r = a;
         r.block_base = uint32_t(b0);
+        if (b0 + kMaxLaunchBlocks < a.n_blocks) r.done_flag = nullptr;  // the last launch signals
         const dim3 grid(uint32_t(std::min<uint64_t>(kMaxLaunchBlocks, a.n_blocks - b0)));
         if (decode && a.compact)
             hipLaunchKernelGGL((rs104_ragged_kernel<true, true>), grid, dim3(kThreads), 0, stream, r);
@@ -841,6 +881,7 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
         for (uint32_t s0 = 0; s0 < a.n_stripes; s0 += step) {
             ApplyArgs b = a;
             b.n_stripes = std::min(step, a.n_stripes - s0);
+            if (s0 + step < a.n_stripes) b.done_flag = nullptr;  // same stream: the last launch signals
             b.in_base += uint64_t(s0) * a.in_stripe;
             b.out_base += uint64_t(s0) * a.out_stripe;
             if (b.masks) b.masks += s0;

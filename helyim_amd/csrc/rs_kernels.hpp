@@ -56,6 +56,13 @@ struct ApplyArgs {
     // the kernels derive (stripe, chunk) in a few scalar ops with no division:
     uint32_t map_q8, map_r8;     // workgroups / 8 and % 8 (XCD eighths remap)
     uint32_t cps_mul, cps_shift; // item / chunks_per_stripe as a multiply-shift (FastDiv)
+    // Optional completion signal (small host calls): the last workgroup of
+    // the launch stores done_seq into done_flag (pinned host memory) after a
+    // system-scope release, so the host spins on it instead of paying
+    // hipStreamSynchronize. done_count: device word, 0 between launches.
+    uint32_t* done_count;
+    uint32_t* done_flag;
+    uint32_t done_seq;
 };
 
 // Ragged RS(10,4) batch (every stripe its own length / stride / mask); all
@@ -82,6 +89,11 @@ struct RaggedArgs {
     uint32_t compact;            // decode: inputs = slots 0..9 at off (the first 10 present
                                  // shards), outputs = slots 0..e-1 at out_off (erased shards)
     uint32_t block_base;         // launcher-internal: first map entry of this launch
+    uint32_t inline_one;         // 1: a single stripe, described by `one` (no items / map in memory)
+    RaggedItem one;
+    uint32_t* done_count;        // optional completion signal, as ApplyArgs
+    uint32_t* done_flag;
+    uint32_t done_seq;
 };
 
 hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t stream);

@@ -389,6 +389,12 @@ int hec_set_host_staging(uint64_t max_bytes);
 /* Host batches on pinned memory: 1 = zero-copy kernels (default), 0 = the
  * copy pipeline. Speed only; identical results. Returns HEC_OK. */
 int hec_set_host_zero_copy(int on);
+/* Host-memory calls coded zero-copy whose input is at most max_bytes learn
+ * that the kernel finished from a flag the kernel's last workgroup stores in
+ * pinned memory (the caller spins on it, up to 200 us, then falls back to a
+ * stream synchronise) instead of hipStreamSynchronize: ~4 us less per small
+ * call. 0 disables. Default 1 MiB. Speed only. Returns HEC_OK. */
+int hec_set_completion_signal(uint64_t max_bytes);
 /* Version string of the library build. */
 const char* hec_version(void);
 /* Name of the kernel a 16-byte-aligned RS(10,4) device batch encode of this

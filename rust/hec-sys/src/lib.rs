@@ -183,6 +183,7 @@ extern "C" {
     pub fn hec_set_workgroup_size(threads: c_int) -> c_int;
     pub fn hec_set_encode_kernel(kind: c_int) -> c_int;
     pub fn hec_set_host_staging(max_bytes: u64) -> c_int;
+    pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;
     pub fn hec_set_host_zero_copy(on: c_int) -> c_int;
     pub fn hec_version() -> *const c_char;
     pub fn hec_encode_kernel_name(shard_len: u64) -> *const c_char;

@@ -133,6 +133,37 @@ def test_host_calls_staged_and_direct(gpu, staging, k, m, zero_copy):
         H.lib.hec_set_host_zero_copy(1)
 
 
+@pytest.mark.parametrize("signal", [1 << 20, 0])
+def test_host_calls_completion_signal(gpu, signal):
+    """Small zero-copy host calls finish on the kernel's own completion flag
+    (hec_set_completion_signal; 0 = hipStreamSynchronize). 400 back-to-back
+    per-call encodes and reconstructs of mixed sizes (one workgroup up to 64
+    workgroups per launch, (10,4) through the fast and ragged kernels, (3,2)
+    through the generic one), each result against the oracle, so a flag seen
+    before the bytes landed, or a counter left non-zero, would show."""
+    import helyim_amd as H
+    rng = np.random.default_rng(4242)
+    H.lib.hec_set_completion_signal(signal)
+    try:
+        for k, m in ((10, 4), (3, 2)):
+            rs, ors = H.ReedSolomon(k, m), O.ReedSolomon(k, m)
+            for it in range(200):
+                L = int(rng.choice([1, 16, 1000, 4096, 4096 + 16, 65536 + 7, 100 * 1024]))
+                ref = [_rand(rng, L) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+                sh = [x.copy() for x in ref]
+                ors.encode(ref)
+                rs.encode(sh)
+                for a, b in zip(sh, ref):
+                    assert np.array_equal(a, b), (k, m, it, L)
+                erased = set(rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False).tolist())
+                got = [None if i in erased else ref[i].copy() for i in range(k + m)]
+                rs.reconstruct(got)
+                for i in range(k + m):
+                    assert np.array_equal(got[i], ref[i]), (k, m, it, L, sorted(erased), i)
+    finally:
+        H.lib.hec_set_completion_signal(1 << 20)
+
+
 def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):
     import torch
     import helyim_amd.batch as B

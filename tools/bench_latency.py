@@ -46,8 +46,11 @@ def main():
         pres = (ctypes.c_uint8 * 14)(*[0 if i in erased else 1 for i in range(14)])
         rlens = (ctypes.c_size_t * 14)(*[0 if i in erased else L for i in range(14)])
         row = {"shard_len": L, "reps": reps}
-        for mode, lim in (("direct", 0), ("staged", 1 << 40)):
+        # staged_sync: completion through hipStreamSynchronize instead of the
+        # kernel's own flag (hec_set_completion_signal(0))
+        for mode, lim, sig in (("direct", 0, 1 << 20), ("staged_sync", 1 << 40, 0), ("staged", 1 << 40, 1 << 20)):
             lib.hec_set_host_staging(lim)
+            lib.hec_set_completion_signal(sig)
             for _ in range(3):
                 assert lib.hec_rs_encode(rs.handle, ptrs, lens, 14) == 0
             t0 = time.perf_counter()
@@ -67,7 +70,8 @@ def main():
             row[mode] = {"encode_us": round(te * 1e6, 1), "reconstruct_us": round(tr * 1e6, 1),
                          "encode_GiB_s": round(10 * L / te / 2**30, 2),
                          "reconstruct_GiB_s": round(10 * L / tr / 2**30, 2), "identical": bool(ok)}
-        lib.hec_set_host_staging(4 << 20)
+        lib.hec_set_host_staging(16 << 20)
+        lib.hec_set_completion_signal(1 << 20)
         cr = max(3, reps // 4)
         b = [f.copy() for f in full]
         t0 = time.perf_counter()

@@ -164,6 +164,32 @@ def test_host_calls_completion_signal(gpu, signal):
         H.lib.hec_set_completion_signal(1 << 20)
 
 
+def test_completion_signal_spin_fallback(gpu):
+    """Calls long enough to outlast the 200 us spin (4 MiB shards, 40 MiB
+    coded zero-copy over PCIe) with the completion signal forced on: the wait
+    falls back to hipStreamSynchronize and must still find the flag set and
+    the bytes right."""
+    import helyim_amd as H
+    rng = np.random.default_rng(99)
+    rs, ors = H.ReedSolomon(10, 4), corc.CReedSolomon(10, 4)
+    L = 4 << 20
+    H.lib.hec_set_completion_signal(1 << 40)
+    H.lib.hec_set_host_staging(1 << 40)  # 40 MiB of input through pinned staging (zero copy)
+    try:
+        for _ in range(3):
+            ref = [_rand(rng, L) for _ in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+            sh = [x.copy() for x in ref]
+            ors.encode(ref)
+            rs.encode(sh)
+            assert all(np.array_equal(a, b) for a, b in zip(sh, ref))
+            got = [None if i in (1, 6, 10, 13) else ref[i].copy() for i in range(14)]
+            rs.reconstruct(got)
+            assert all(np.array_equal(a, b) for a, b in zip(got, ref))
+    finally:
+        H.lib.hec_set_completion_signal(1 << 20)
+        H.lib.hec_set_host_staging(16 << 20)
+
+
 def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):
     import torch
     import helyim_amd.batch as B

@@ -171,6 +171,7 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     ra.tabs = gd->decode_dense.tabs;
     ra.lut = gd->decode_dense.lut;
     ra.compact = 1;
+    ra.xcd_remap = launch_config().xcd_remap == 1 ? 1u : 0u;
     if (items.size() == 1) {  // one stripe (a per-call reconstruct): descriptor as a kernel argument
         ra.inline_one = 1;
         ra.one = items[0];
@@ -280,6 +281,13 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
 namespace hec {
 namespace {
 
+// Workgroups of one ragged stripe: none for a decode of a stripe whose 14
+// shards are all present (upstream's no-op), so those launch nothing.
+uint64_t ragged_chunks(const hec_stripe_desc& d, bool decode, uint32_t chunk_bytes) {
+    if (decode && (d.present_mask & 0x3FFFu) == 0x3FFFu) return 0;
+    return (uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes;
+}
+
 // Device-resident ragged batches: stripe descriptors come from the host, data
 // stays in HBM. Descriptors -> RaggedItems + workgroup map in pinned staging,
 // uploaded on the caller's stream ahead of the kernel.
@@ -302,7 +310,7 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
             return fail(HEC_ERR_INVALID_ARGUMENT, "stripe " + std::to_string(j) +
                                                       ": offset/stride must be 16-byte aligned, stride >= len");
         // 64-bit: a shard_len near 2^32 must not wrap to 0 or 1 chunks
-        n_blocks += (uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes;
+        n_blocks += ragged_chunks(d, decode, chunk_bytes);
         if (n_blocks > UINT32_MAX) return fail(HEC_ERR_INVALID_ARGUMENT, "ragged batch above 2^32 workgroups");
     }
     if (n == 0) return HEC_OK;
@@ -325,7 +333,7 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     uint32_t first = 0;
     for (uint32_t j = 0; j < n; ++j) {
         const hec_stripe_desc& d = descs[j];
-        const uint32_t chunks = uint32_t((uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes);
+        const uint32_t chunks = uint32_t(ragged_chunks(d, decode, chunk_bytes));
         items[j] = RaggedItem{d.offset, d.shard_stride, d.shard_len, d.present_mask, first, 0, 0};
         std::fill(block_item + first, block_item + first + chunks, j);
         first += chunks;
@@ -339,6 +347,14 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     ra.tabs = decode ? gd->decode_dense.tabs : gd->encode.tabs;
     ra.lut = decode ? gd->decode_dense.lut : nullptr;
     ra.bad_count = d_bad;
+    // XCD eighths for the ragged decode (+2% on the bench batch, with the
+    // no-op skip +10% on the mixed workload's decode); the bit-sliced ragged
+    // encode measured 1% slower with it (profiles/r02/ab_ragged_remap_skip.jsonl)
+    ra.xcd_remap = decode && cfg.xcd_remap == 1 ? 1u : 0u;
+    if (n_blocks == 0) {  // every stripe already complete (upstream no-op)
+        HEC_HIP(hipEventRecord(slot.free, stream));
+        return HEC_OK;
+    }
     if (bitslice)
         HEC_HIP(launch_rs104_bs_ragged(ra, stream));
     else

@@ -658,6 +658,18 @@ __global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
+// Map entry of this workgroup: with xcd_remap, XCD x = blockIdx % 8 takes
+// the x-th eighth of the launch's entries, so the workgroups sharing an XCD
+// (and its L2) stream consecutive chunks, as in the strided kernels.
+__device__ __forceinline__ uint32_t ragged_block(const RaggedArgs& a) {
+    uint32_t b = blockIdx.x;
+    if (a.xcd_remap) {
+        const uint32_t x = b & 7u;
+        b = x * a.map_q8 + (x < a.map_r8 ? x : a.map_r8) + (b >> 3);
+    }
+    return b + a.block_base;
+}
+
 // Descriptor of the stripe workgroup blk works on: the kernel-argument copy
 // for a one-stripe launch, else the workgroup map and item table (scalar loads).
 __device__ __forceinline__ RaggedItem ragged_item(const RaggedArgs& a, uint32_t blk) {
@@ -669,7 +681,7 @@ __device__ __forceinline__ RaggedItem ragged_item(const RaggedArgs& a, uint32_t 
 // Ragged encode with every stripe length a multiple of 8 KiB: workgroup ->
 // stripe map as rs104_ragged_kernel, one 8 KiB column range per workgroup.
 __global__ __launch_bounds__(kThreads) void rs104_bs_ragged_kernel(RaggedArgs a) {
-    const uint32_t blk = blockIdx.x + a.block_base;
+    const uint32_t blk = ragged_block(a);
     const RaggedItem it = ragged_item(a, blk);
     const uint64_t off = it.off, stride = it.shard_stride;
     const uint32_t first = it.first_block;
@@ -684,6 +696,8 @@ hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
         r.block_base = uint32_t(b0);
         if (b0 + kMaxLaunchBlocks < a.n_blocks) r.done_flag = nullptr;  // the last launch signals
         const uint32_t nb = uint32_t(std::min<uint64_t>(kMaxLaunchBlocks, a.n_blocks - b0));
+        r.map_q8 = nb / 8;
+        r.map_r8 = nb % 8;
         hipLaunchKernelGGL(rs104_bs_ragged_kernel, dim3(nb), dim3(kThreads), 0, stream, r);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -739,7 +753,7 @@ static hipError_t launch_rs104_bs_cfg(const ApplyArgs& a, const LaunchConfig& cf
 // lays stripes out back to back and passes a workgroup -> stripe map.
 template <bool DEC, bool COMPACT>
 __global__ __launch_bounds__(kThreads) void rs104_ragged_kernel(RaggedArgs a) {
-    const uint32_t blk = blockIdx.x + a.block_base;
+    const uint32_t blk = ragged_block(a);
     // one stripe (a per-call host reconstruct): its descriptor is a kernel
     // argument, so the launch needs no metadata upload and no dependent loads
     const RaggedItem it = ragged_item(a, blk);
@@ -757,6 +771,8 @@ hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t str
         r.block_base = uint32_t(b0);
         if (b0 + kMaxLaunchBlocks < a.n_blocks) r.done_flag = nullptr;  // the last launch signals
         const dim3 grid(uint32_t(std::min<uint64_t>(kMaxLaunchBlocks, a.n_blocks - b0)));
+        r.map_q8 = grid.x / 8;
+        r.map_r8 = grid.x % 8;
         if (decode && a.compact)
             hipLaunchKernelGGL((rs104_ragged_kernel<true, true>), grid, dim3(kThreads), 0, stream, r);
         else if (decode)

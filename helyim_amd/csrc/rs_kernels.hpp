@@ -89,6 +89,8 @@ struct RaggedArgs {
     uint32_t compact;            // decode: inputs = slots 0..9 at off (the first 10 present
                                  // shards), outputs = slots 0..e-1 at out_off (erased shards)
     uint32_t block_base;         // launcher-internal: first map entry of this launch
+    uint32_t xcd_remap;          // 1: XCD eighths of each launch's workgroups (speed only)
+    uint32_t map_q8, map_r8;     // launcher-internal: that launch's workgroups / 8 and % 8
     uint32_t inline_one;         // 1: a single stripe, described by `one` (no items / map in memory)
     RaggedItem one;
     uint32_t* done_count;        // optional completion signal, as ApplyArgs

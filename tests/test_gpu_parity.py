@@ -514,6 +514,16 @@ def test_ragged_device_batch(gpu, lengths):
         if j == 0:
             continue
         assert torch.equal(buf[o: o + 14 * st], good[o: o + 14 * st]), j
+    # every stripe complete: upstream's no-op, and the call launches no
+    # workgroup at all (all-present stripes get none); poisoned parity stays
+    for d in descs:
+        d[3] = full
+    buf[descs[1][0] + 12 * descs[1][1]] ^= 0xFF
+    snap = buf.clone()
+    bad.zero_()
+    B.reconstruct_ragged(rs, buf, descs, bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0 and torch.equal(buf, snap)
 
 
 def test_concurrent_host_calls(gpu):

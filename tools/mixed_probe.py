@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stripes", type=int, default=512)
+    ap.add_argument("--uniform", type=int, default=0,
+                    help="E > 0: every stripe 1 MiB with exactly E random erasures (the bench batch through "
+                         "the ragged kernels; compare with the strided kernels' times)")
     args = ap.parse_args()
     import torch
     import helyim_amd as H
@@ -34,6 +37,9 @@ def main():
     n = args.stripes
     Ls = rng.choice(lens, n)
     es = rng.integers(0, 5, n)
+    if args.uniform:
+        Ls = np.full(n, 1 << 20)
+        es = np.full(n, args.uniform)
     full = (1 << 14) - 1
     masks = [full & ~int(sum(1 << int(i) for i in rng.choice(14, int(e), replace=False))) for e in es]
     descs, off = [], 0
@@ -60,7 +66,11 @@ def main():
         enc = np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)])
         dec = np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)])
         wall = ev[0].elapsed_time(ev[-1]) / args.reps
-        print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "round": r, "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
+        enc_b = sum(14 * d[2] for d in descs)
+        dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
+        print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n, "round": r,
+                          "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
+                          "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3), "dec_ms": round(float(dec), 3),
                           "payload_GiB": round(payload / 2**30, 3)}), flush=True)
 

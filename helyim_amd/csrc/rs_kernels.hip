@@ -168,12 +168,13 @@ typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 // accumulator by three 3-input XORs (v_bitop3) instead of four ops.
 // nrows (wave-uniform, <= R): rows at or past it skip their math (a decode
 // with e < 4 erasures; scalar branches, the tables keep their 4-row stride).
-template <int R>
-__device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R], const u32x4 d0, const u32x4 d1, cu32p tab0, cu32p tab1,
+template <int R, typename V = u32x4>
+__device__ __forceinline__ void gf_mac2(V (&acc)[R], const V d0, const V d1, cu32p tab0, cu32p tab1,
                                         uint32_t nrows = R) {
-    uint32_t s[2][3][4];
+    constexpr int W = int(sizeof(V) / 4);  // dwords per lane vector
+    uint32_t s[2][3][W];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < W; ++w) {
         const uint32_t x0 = d0[w], x1 = d1[w];
         s[0][0][w] = x0 & 0x07070707u;
         s[0][1][w] = (x0 >> 3) & 0x07070707u;
@@ -203,7 +204,7 @@ __device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R], const u32x4 d0, const u
         const uint32_t b0l = tbw[r * 5 + 0], b0h = tbw[r * 5 + 1], b1l = tbw[r * 5 + 2], b1h = tbw[r * 5 + 3],
                        b2 = tbw[r * 5 + 4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < W; ++w) {
             const uint32_t p0 = __builtin_amdgcn_perm(a0h, a0l, s[0][0][w]);
             const uint32_t p1 = __builtin_amdgcn_perm(a1h, a1l, s[0][1][w]);
             const uint32_t p2 = __builtin_amdgcn_perm(a2, a2, s[0][2][w]);
@@ -521,6 +522,67 @@ __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
+// The decode with 8 or 4 bytes per lane (hec_set_decode_vector_bytes; 2 or
+// 1 KiB column range per workgroup, dwordx2 / dword streams): less math per
+// wave between its loads and its stores, fewer VGPRs (54 at 8 B). Shard
+// length a multiple of the column range, shipped mapping only.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x1 __attribute__((ext_vector_type(1)));
+template <typename V>
+__global__ __launch_bounds__(kThreads) void rs104_dec_narrow_kernel(ApplyArgs a) {
+    constexpr int K = 10, N = 14, R = 4, VB = int(sizeof(V));
+    uint32_t stripe, chunk;
+    fast_item<true>(a, a.chunks_per_stripe, stripe, chunk);
+    const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
+    const uint32_t present = __builtin_popcount(mask);
+    if (present < K || present == N) {
+        if (present < K && chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
+    } else {
+        const uint32_t nout = N - present;
+        uint32_t in_id[K], out_id[R];
+        uint32_t m = mask;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {  // first K present shards, ascending
+            in_id[i] = __builtin_ctz(m);
+            m &= m - 1;
+        }
+        uint32_t e = ~mask & ((1u << N) - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {  // erased shards, ascending
+            out_id[r] = e ? __builtin_ctz(e) : 0;
+            e &= e - 1;
+        }
+        uint32_t plan = as_const(a.lut)[mask];  // first used after the data loads
+        const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
+        uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
+        const uint32_t o = chunk * (kThreads * VB) + threadIdx.x * VB;
+        V d[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            d[i] = __builtin_nontemporal_load(
+                (const __attribute__((address_space(1))) V*)((gcu8p)(in_b + uint64_t(in_id[i]) * a.in_shard) + o));
+        __builtin_amdgcn_sched_barrier(0);  // all ten loads in flight before the math
+        asm volatile("" : "+s"(plan));
+        cu32p tab = as_const(a.tabs) + plan * (K * R * 5);
+        V acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = V(0u);
+#pragma unroll
+        for (int i = 0; i < K; i += 2)
+            gf_mac2<R, V>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int w = 0; w < VB / 4; ++w) asm volatile("" ::"v"(acc[r][w]));
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r < int(nout))
+                __builtin_nontemporal_store(
+                    acc[r], (__attribute__((address_space(1))) V*)((gu8p)(out_b + uint64_t(out_id[r]) * a.out_shard) + o));
+    }
+    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
+}
+
 // Two 4 KiB chunks per workgroup (launch config vec_per_thread = 2; shard
 // length a multiple of 8 KiB): each lane issues the 20 loads of both chunks,
 // then does the math of the first while the second's loads are in flight.
@@ -829,6 +891,21 @@ static hipError_t launch_rs104_pair(ApplyArgs a, const LaunchConfig& cfg, hipStr
 
 template <bool DEC, bool XORONLY>
 static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
+    const uint64_t narrow = uint64_t(kThreads) * uint64_t(cfg.dec_vec_bytes);  // column range per workgroup
+    if (DEC && !XORONLY && cfg.dec_vec_bytes < 16 && cfg.vec_per_thread == 1 && a.len % narrow == 0 &&
+        fast_map_ok(cfg, a.len) && cfg.wg_threads == kThreads) {
+        ApplyArgs b = a;
+        b.chunks_per_stripe = uint32_t(a.len / narrow);
+        b.n_items = uint64_t(b.chunks_per_stripe) * a.n_stripes;
+        if (b.n_items == 0) return hipSuccess;
+        b.xcd_remap = uint32_t(cfg.xcd_remap);
+        set_fast_map(b, b.n_items, b.chunks_per_stripe);
+        if (cfg.dec_vec_bytes == 8)
+            hipLaunchKernelGGL(rs104_dec_narrow_kernel<u32x2>, dim3(uint32_t(b.n_items)), dim3(kThreads), 0, stream, b);
+        else
+            hipLaunchKernelGGL(rs104_dec_narrow_kernel<u32x1>, dim3(uint32_t(b.n_items)), dim3(kThreads), 0, stream, b);
+        return hipGetLastError();
+    }
     if (cfg.vec_per_thread == 2 && a.len % (2 * uint64_t(kThreads) * kVecBytes) == 0)
         return launch_rs104_pair<DEC, XORONLY>(a, cfg, stream);
     switch (cfg.wg_threads) {
@@ -872,6 +949,10 @@ const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
     if (!rs104_fast_ok(len, cfg)) return "rs_apply_kernel<10> (table lookup)";
     if (cfg.mode == 1) return "rs104_kernel<DEC=true, XORONLY=true> (diagnostic)";
     if (cfg.vec_per_thread == 2) return "rs104_pair_kernel<DEC=true> (table lookup)";
+    if (cfg.dec_vec_bytes < 16 && len % (uint64_t(kThreads) * cfg.dec_vec_bytes) == 0 && fast_map_ok(cfg, len) &&
+        cfg.wg_threads == kThreads)
+        return cfg.dec_vec_bytes == 8 ? "rs104_dec_narrow_kernel<8 B per lane> (table lookup)"
+                                      : "rs104_dec_narrow_kernel<4 B per lane> (table lookup)";
     return "rs104_kernel<DEC=true> (table lookup)";
 }
 

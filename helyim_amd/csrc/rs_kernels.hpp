@@ -113,6 +113,8 @@ struct LaunchConfig {
     int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
     int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
     int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
+    int dec_vec_bytes = 8;       // RS(10,4) decode bytes per lane per shard: 8 (default: dwordx2, 2 KiB
+                                 // per workgroup, on shard lengths a multiple of 2 KiB), 16 or 4 (speed only)
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
                                  // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
                                  // multiply (speed only)

@@ -375,6 +375,10 @@ int hec_set_kernel_mode(int mode);
  * workgroup), 512 or 1024 (8 / 16 KiB per shard per workgroup); 128 applies to
  * the bit-sliced encode only (others use 256). Speed only. */
 int hec_set_workgroup_size(int threads);
+/* RS(10,4) device decode bytes per lane per shard: 8 (default; 2 KiB per
+ * workgroup, on shard lengths that are a multiple of 2 KiB, others take 16),
+ * 16 (4 KiB per workgroup) or 4 (1 KiB). Speed only. */
+int hec_set_decode_vector_bytes(int bytes);
 /* RS(10,4) encode kernel on shard lengths that are a multiple of
  * 32 x workgroup size bytes (8 KiB at 256 threads): 1 = bit-sliced (bytes
  * transposed into bit planes, the fixed parity matrix applied as a generated

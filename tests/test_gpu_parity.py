@@ -374,11 +374,12 @@ def test_batch_reconstruct_every_pattern(gpu):
     assert torch.equal(t, good)
 
 
-@pytest.mark.parametrize("vec", [1, 2])
-@pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192 + 16])
+@pytest.mark.parametrize("vec", ["16B", 2, "8B", "4B"])
+@pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192 + 16, 2048 * 5])
 def test_decode_kernels_every_pattern(gpu, vec, L):
-    """The RS(10,4) decode kernels (one 4 KiB chunk per workgroup, or the
-    pair kernel's two) with all ten loads issued before the math: all 1470
+    """The RS(10,4) decode kernels (16 bytes per lane over one 4 KiB chunk per
+    workgroup, the pair kernel's two chunks, or 8 / 4 bytes per lane over
+    2 / 1 KiB) with all ten loads issued before the math: all 1470
     patterns (erased slots poisoned), plus an all-present stripe (no-op) and
     two with too few present (skipped, counted), vs the originals; the
     kernel-name report follows the launch configuration."""
@@ -399,14 +400,18 @@ def test_decode_kernels_every_pattern(gpu, vec, L):
     masks[-2] = (1 << 14) - 1 - 0b11111           # 9 present
     masks[-1] = (1 << 14) - 1 - (0b1111 << 10) - 1  # 9 present, all parity gone
     try:
-        B.set_launch_config(vec_per_thread=vec)
+        B.set_launch_config(vec_per_thread=2 if vec == 2 else 1)
+        H.lib.hec_set_decode_vector_bytes({"8B": 8, "4B": 4}.get(vec, 16))
         name = H.lib.hec_decode_kernel_name(L).decode()
         assert ("pair" in name) == (vec == 2 and L % 8192 == 0), name
+        assert ("8 B per lane" in name) == (vec == "8B" and L % 2048 == 0), name
+        assert ("4 B per lane" in name) == (vec == "4B" and L % 1024 == 0), name
         bad = torch.zeros(1, dtype=torch.int32, device="cuda")
         B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda(), bad)
         torch.cuda.synchronize()
     finally:
         B.set_launch_config()
+        H.lib.hec_set_decode_vector_bytes(8)
     assert int(bad.item()) == 2
     assert torch.equal(t, good)
 

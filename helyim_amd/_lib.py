@@ -90,6 +90,7 @@ SIGNATURES = {
     "hec_set_completion_signal": (_I, [ctypes.c_uint64]),
     "hec_set_workgroup_size": (_I, [_I]),
     "hec_set_decode_vector_bytes": (_I, [_I]),
+    "hec_set_encode_vector_bytes": (_I, [_I]),
     "hec_set_encode_kernel": (_I, [_I]),
     "hec_set_host_zero_copy": (_I, [_I]),
     "hec_set_xcd_parts": (_I, [_I]),

@@ -687,6 +687,13 @@ int hec_set_decode_vector_bytes(int bytes) {
     return HEC_OK;
 }
 
+int hec_set_encode_vector_bytes(int bytes) {
+    if (bytes != 4 && bytes != 8 && bytes != 16)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "encode vector bytes must be 4, 8 or 16");
+    update_launch_config([&](LaunchConfig& c) { c.enc_vec_bytes = bytes; });
+    return HEC_OK;
+}
+
 int hec_set_encode_kernel(int kind) {
     if (kind != 0 && kind != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0 or 1");
     update_launch_config([&](LaunchConfig& c) { c.bitslice = kind; });

@@ -522,28 +522,33 @@ __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
-// The decode with 8 or 4 bytes per lane (hec_set_decode_vector_bytes; 2 or
-// 1 KiB column range per workgroup, dwordx2 / dword streams): less math per
-// wave between its loads and its stores, fewer VGPRs (54 at 8 B). Shard
-// length a multiple of the column range, shipped mapping only.
+// RS(10,4) with 8 or 4 bytes per lane (hec_set_decode_vector_bytes /
+// hec_set_encode_vector_bytes; 2 or 1 KiB column range per workgroup,
+// dwordx2 / dword streams): less math per wave between its loads and its
+// stores, fewer VGPRs (54 for the 8 B decode), more waves per SIMD. The
+// default decode on shards that are a multiple of 2 KiB.
+// Encode (DEC=false: inputs 0..9, outputs 0..3) and the XOR-only twin
+// (XORONLY: same traffic, no GF math) are measurement forms.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x1 __attribute__((ext_vector_type(1)));
-template <typename V>
-__global__ __launch_bounds__(kThreads) void rs104_dec_narrow_kernel(ApplyArgs a) {
+template <bool DEC, bool XORONLY, typename V>
+__global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
     constexpr int K = 10, N = 14, R = 4, VB = int(sizeof(V));
     uint32_t stripe, chunk;
     fast_item<true>(a, a.chunks_per_stripe, stripe, chunk);
-    const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
-    const uint32_t present = __builtin_popcount(mask);
-    if (present < K || present == N) {
+    uint32_t in_id[K], out_id[R];
+    uint32_t nout = R, plan = 0;
+    bool work = true;
+    if constexpr (DEC) {
+        const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
+        const uint32_t present = __builtin_popcount(mask);
         if (present < K && chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
-    } else {
-        const uint32_t nout = N - present;
-        uint32_t in_id[K], out_id[R];
+        work = present >= K && present < N;  // too few: skipped + counted; all present: upstream no-op
+        nout = N - present;
         uint32_t m = mask;
 #pragma unroll
         for (int i = 0; i < K; ++i) {  // first K present shards, ascending
-            in_id[i] = __builtin_ctz(m);
+            in_id[i] = m ? __builtin_ctz(m) : 0;
             m &= m - 1;
         }
         uint32_t e = ~mask & ((1u << N) - 1);
@@ -552,7 +557,14 @@ __global__ __launch_bounds__(kThreads) void rs104_dec_narrow_kernel(ApplyArgs a)
             out_id[r] = e ? __builtin_ctz(e) : 0;
             e &= e - 1;
         }
-        uint32_t plan = as_const(a.lut)[mask];  // first used after the data loads
+        if (work) plan = as_const(a.lut)[mask];  // first used after the data loads
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) in_id[i] = i;
+#pragma unroll
+        for (int r = 0; r < R; ++r) out_id[r] = r;
+    }
+    if (work) {
         const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
         uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
         const uint32_t o = chunk * (kThreads * VB) + threadIdx.x * VB;
@@ -561,15 +573,24 @@ __global__ __launch_bounds__(kThreads) void rs104_dec_narrow_kernel(ApplyArgs a)
         for (int i = 0; i < K; ++i)
             d[i] = __builtin_nontemporal_load(
                 (const __attribute__((address_space(1))) V*)((gcu8p)(in_b + uint64_t(in_id[i]) * a.in_shard) + o));
+#if HEC_LOADS_FIRST
         __builtin_amdgcn_sched_barrier(0);  // all ten loads in flight before the math
+#endif
         asm volatile("" : "+s"(plan));
         cu32p tab = as_const(a.tabs) + plan * (K * R * 5);
         V acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = V(0u);
+        if constexpr (XORONLY) {
 #pragma unroll
-        for (int i = 0; i < K; i += 2)
-            gf_mac2<R, V>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r] ^= d[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; i += 2)
+                gf_mac2<R, V>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -891,19 +912,22 @@ static hipError_t launch_rs104_pair(ApplyArgs a, const LaunchConfig& cfg, hipStr
 
 template <bool DEC, bool XORONLY>
 static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t narrow = uint64_t(kThreads) * uint64_t(cfg.dec_vec_bytes);  // column range per workgroup
-    if (DEC && !XORONLY && cfg.dec_vec_bytes < 16 && cfg.vec_per_thread == 1 && a.len % narrow == 0 &&
-        fast_map_ok(cfg, a.len) && cfg.wg_threads == kThreads) {
+    const int vb = DEC ? cfg.dec_vec_bytes : cfg.enc_vec_bytes;
+    const uint64_t narrow = uint64_t(kThreads) * uint64_t(vb);  // column range per workgroup
+    if (vb < 16 && cfg.vec_per_thread == 1 && a.len % narrow == 0 && fast_map_ok(cfg, a.len) &&
+        cfg.wg_threads == kThreads) {
         ApplyArgs b = a;
         b.chunks_per_stripe = uint32_t(a.len / narrow);
         b.n_items = uint64_t(b.chunks_per_stripe) * a.n_stripes;
         if (b.n_items == 0) return hipSuccess;
         b.xcd_remap = uint32_t(cfg.xcd_remap);
         set_fast_map(b, b.n_items, b.chunks_per_stripe);
-        if (cfg.dec_vec_bytes == 8)
-            hipLaunchKernelGGL(rs104_dec_narrow_kernel<u32x2>, dim3(uint32_t(b.n_items)), dim3(kThreads), 0, stream, b);
+        if (vb == 8)
+            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x2>), dim3(uint32_t(b.n_items)), dim3(kThreads), 0,
+                               stream, b);
         else
-            hipLaunchKernelGGL(rs104_dec_narrow_kernel<u32x1>, dim3(uint32_t(b.n_items)), dim3(kThreads), 0, stream, b);
+            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x1>), dim3(uint32_t(b.n_items)), dim3(kThreads), 0,
+                               stream, b);
         return hipGetLastError();
     }
     if (cfg.vec_per_thread == 2 && a.len % (2 * uint64_t(kThreads) * kVecBytes) == 0)
@@ -951,8 +975,8 @@ const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
     if (cfg.vec_per_thread == 2) return "rs104_pair_kernel<DEC=true> (table lookup)";
     if (cfg.dec_vec_bytes < 16 && len % (uint64_t(kThreads) * cfg.dec_vec_bytes) == 0 && fast_map_ok(cfg, len) &&
         cfg.wg_threads == kThreads)
-        return cfg.dec_vec_bytes == 8 ? "rs104_dec_narrow_kernel<8 B per lane> (table lookup)"
-                                      : "rs104_dec_narrow_kernel<4 B per lane> (table lookup)";
+        return cfg.dec_vec_bytes == 8 ? "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)"
+                                      : "rs104_narrow_kernel<DEC=true, 4 B per lane> (table lookup)";
     return "rs104_kernel<DEC=true> (table lookup)";
 }
 
@@ -961,6 +985,10 @@ const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
         return cfg.mode == 1 ? "rs_apply_kernel<10, XORONLY=true> (diagnostic)" : "rs_apply_kernel<10> (table lookup)";
     if (cfg.mode == 1) return "rs104_kernel<DEC=false, XORONLY=true> (diagnostic)";
     if (rs104_bitslice_ok(len, cfg)) return "rs104_bs_encode_kernel (bit-sliced)";
+    if (cfg.enc_vec_bytes < 16 && len % (uint64_t(kThreads) * cfg.enc_vec_bytes) == 0 && fast_map_ok(cfg, len) &&
+        cfg.wg_threads == kThreads)
+        return cfg.enc_vec_bytes == 8 ? "rs104_narrow_kernel<DEC=false, 8 B per lane> (table lookup)"
+                                      : "rs104_narrow_kernel<DEC=false, 4 B per lane> (table lookup)";
     if (cfg.vec_per_thread == 2) return "rs104_pair_kernel<DEC=false> (table lookup)";
     return "rs104_kernel<DEC=false> (table lookup)";
 }

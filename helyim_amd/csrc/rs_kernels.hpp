@@ -115,6 +115,7 @@ struct LaunchConfig {
     int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
     int dec_vec_bytes = 8;       // RS(10,4) decode bytes per lane per shard: 8 (default: dwordx2, 2 KiB
                                  // per workgroup, on shard lengths a multiple of 2 KiB), 16 or 4 (speed only)
+    int enc_vec_bytes = 16;      // RS(10,4) table encode bytes per lane per shard: 16 (default), 8 or 4 (speed only)
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
                                  // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
                                  // multiply (speed only)

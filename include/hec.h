@@ -379,6 +379,9 @@ int hec_set_workgroup_size(int threads);
  * workgroup, on shard lengths that are a multiple of 2 KiB, others take 16),
  * 16 (4 KiB per workgroup) or 4 (1 KiB). Speed only. */
 int hec_set_decode_vector_bytes(int bytes);
+/* Same for the RS(10,4) table-lookup encode (the encodes the bit-sliced
+ * kernel does not take): 16 (default), 8 or 4 bytes per lane. Speed only. */
+int hec_set_encode_vector_bytes(int bytes);
 /* RS(10,4) encode kernel on shard lengths that are a multiple of
  * 32 x workgroup size bytes (8 KiB at 256 threads): 1 = bit-sliced (bytes
  * transposed into bit planes, the fixed parity matrix applied as a generated

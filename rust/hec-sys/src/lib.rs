@@ -182,6 +182,7 @@ extern "C" {
     pub fn hec_set_kernel_mode(mode: c_int) -> c_int;
     pub fn hec_set_workgroup_size(threads: c_int) -> c_int;
     pub fn hec_set_decode_vector_bytes(bytes: c_int) -> c_int;
+    pub fn hec_set_encode_vector_bytes(bytes: c_int) -> c_int;
     pub fn hec_set_encode_kernel(kind: c_int) -> c_int;
     pub fn hec_set_host_staging(max_bytes: u64) -> c_int;
     pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;

@@ -221,6 +221,32 @@ def test_batch_encode_vs_oracle(gpu, L):
     assert np.array_equal(host[:, 10:], ref)
 
 
+@pytest.mark.parametrize("ev", [8, 4])
+@pytest.mark.parametrize("L", [1024, 2048, 6144, 65536, 4096 + 16])
+def test_narrow_table_encode_vs_oracle(gpu, ev, L):
+    """hec_set_encode_vector_bytes(8 / 4) with the bit-sliced kernel off: the
+    table encode at 8 or 4 bytes per lane (rs104_narrow_kernel<DEC=false>) on
+    lengths that are a multiple of its column range, the 16-byte kernel on the
+    others; parity against the C oracle, the kernel-name report in step."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    t = _stripes(7, L)
+    H.lib.hec_set_encode_kernel(0)
+    H.lib.hec_set_encode_vector_bytes(ev)
+    try:
+        name = H.lib.hec_encode_kernel_name(L).decode()
+        assert (f"{ev} B per lane" in name) == (L % (256 * ev) == 0), name
+        B.encode_batch(rs, t)
+        torch.cuda.synchronize()
+    finally:
+        H.lib.hec_set_encode_kernel(1)
+        H.lib.hec_set_encode_vector_bytes(16)
+    host = t.cpu().numpy()
+    assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
+
+
 @pytest.mark.parametrize("vec,max_blocks,remap,bpc,wg", [
     (1, 0, 0, 0, 256), (1, 0, 1, 0, 256), (1, 0, 16, 0, 256), (1, 0, 256, 3, 256), (1, 97, 1, 0, 256),
     (2, 0, 1, 0, 256), (2, 97, 0, 0, 256), (4, 0, 64, 0, 256), (4, 97, 1, 2, 256),

@@ -36,10 +36,10 @@ def load(path, counter):
 def split(per_kernel):
     """encode / decode series by kernel name: the encode kernel is
     rs104_bs_encode_kernel (bit-sliced) or rs104_kernel<false, ...>, decode is
-    rs104_kernel<true, ...> or rs104_dec_narrow_kernel; a single generic kernel alternates encode (even)
+    rs104_kernel<true, ...> or rs104_narrow_kernel<true, ...>; a single generic kernel alternates encode (even)
     / decode (odd)."""
     enc = [k for k in per_kernel if "rs104_bs_encode_kernel" in k or "rs104_kernel<false" in k]
-    dec = [k for k in per_kernel if "rs104_kernel<true" in k or "rs104_dec_narrow_kernel" in k]
+    dec = [k for k in per_kernel if "rs104_kernel<true" in k or "rs104_narrow_kernel<true" in k]
     if enc and dec:
         return per_kernel[enc[0]], per_kernel[dec[0]], [enc[0], dec[0]]
     (k, v), = per_kernel.items()

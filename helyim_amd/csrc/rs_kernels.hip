@@ -914,8 +914,10 @@ template <bool DEC, bool XORONLY>
 static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
     const int vb = DEC ? cfg.dec_vec_bytes : cfg.enc_vec_bytes;
     const uint64_t narrow = uint64_t(kThreads) * uint64_t(vb);  // column range per workgroup
+    // (launch_apply sizes its stripe ranges for 4 KiB chunks; a narrow launch
+    // that would pass kMaxLaunchBlocks workgroups takes the 16-byte kernel)
     if (vb < 16 && cfg.vec_per_thread == 1 && a.len % narrow == 0 && fast_map_ok(cfg, a.len) &&
-        cfg.wg_threads == kThreads) {
+        cfg.wg_threads == kThreads && (a.len / narrow) * a.n_stripes <= kMaxLaunchBlocks) {
         ApplyArgs b = a;
         b.chunks_per_stripe = uint32_t(a.len / narrow);
         b.n_items = uint64_t(b.chunks_per_stripe) * a.n_stripes;

@@ -434,10 +434,13 @@ int Completion::wait(hipStream_t s) {
     while (__atomic_load_n(host, __ATOMIC_ACQUIRE) != seq) {
         if ((++spins & 255) == 0 &&
             std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
-            HEC_HIP(hipStreamSynchronize(s));
-            if (__atomic_load_n(host, __ATOMIC_ACQUIRE) != seq)
-                return fail(HEC_ERR_HIP, "kernel finished without its completion signal");
-            return HEC_OK;
+            const hipError_t e = hipStreamSynchronize(s);
+            if (e == hipSuccess && __atomic_load_n(host, __ATOMIC_ACQUIRE) == seq) return HEC_OK;
+            // a launch that did not finish every workgroup leaves the arrival
+            // count non-zero: clear it so the next signalled call counts right
+            (void)hipMemset(count, 0, 64);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize (completion fallback)");
+            return fail(HEC_ERR_HIP, "kernel finished without its completion signal");
         }
     }
     return HEC_OK;

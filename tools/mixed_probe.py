@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stripes", type=int, default=512)
+    ap.add_argument("--grouped", action="store_true",
+                    help="also time the same stripes as one strided batch per shard length (7 encode + 7 "
+                         "reconstruct launches): the ceiling a length-grouped ragged launch could reach")
     ap.add_argument("--uniform", type=int, default=0,
                     help="E > 0: every stripe 1 MiB with exactly E random erasures (the bench batch through "
                          "the ragged kernels; compare with the strided kernels' times)")
@@ -73,6 +76,41 @@ def main():
                           "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3), "dec_ms": round(float(dec), 3),
                           "payload_GiB": round(payload / 2**30, 3)}), flush=True)
+    if args.grouped:
+        del dev
+        grouped(rs, B, torch, Ls, masks, args.rounds, args.reps)
+
+
+def grouped(rs, B, torch, Ls, masks, rounds, reps):
+    """The mixed batch as one strided [n_L][14][L] tensor per length."""
+    full = (1 << 14) - 1
+    groups = []
+    for L in sorted(set(int(x) for x in Ls)):
+        idx = [s for s in range(len(Ls)) if int(Ls[s]) == L]
+        t = torch.empty((len(idx), 14, L), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(t, 10 * L, 0x5EED0000)
+        m = torch.tensor([masks[s] for s in idx], dtype=torch.int32, device="cuda")
+        groups.append((t, m))
+    enc_b = sum(14 * t.shape[0] * t.shape[2] for t, _ in groups)
+    dec_b = sum((24 - bin(int(x)).count("1")) * t.shape[2] for t, m in groups for x in m.tolist() if x != full)
+    st = torch.cuda.current_stream()
+    for r in range(rounds):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        enc = dec = 0.0
+        for _ in range(reps):
+            e[0].record(st)
+            for t, _ in groups:
+                B.encode_batch(rs, t)
+            e[1].record(st)
+            for t, m in groups:
+                B.reconstruct_batch(rs, t, m)
+            e[2].record(st)
+            torch.cuda.synchronize()
+            enc += e[0].elapsed_time(e[1]) / reps
+            dec += e[1].elapsed_time(e[2]) / reps
+        print(json.dumps({"grouped_strided": True, "round": r, "enc_TBps": round(enc_b / enc / 1e9, 3),
+                          "dec_TBps": round(dec_b / dec / 1e9, 3), "enc_ms": round(enc, 3), "dec_ms": round(dec, 3)}),
+              flush=True)
 
 
 if __name__ == "__main__":

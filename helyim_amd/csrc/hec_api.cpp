@@ -365,7 +365,7 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
 // Per-device scratch for host-memory calls
 // ---------------------------------------------------------------------------
 static std::mutex g_scratch_mu;
-static std::map<int, std::unique_ptr<Scratch>> g_scratch;
+static std::map<int, std::unique_ptr<SlotPool<Scratch>>> g_scratch;  // per device, process lifetime
 
 int Scratch::reserve(size_t bytes) {
     if (bytes <= dcap) return HEC_OK;
@@ -446,19 +446,23 @@ int Completion::wait(hipStream_t s) {
     return HEC_OK;
 }
 
-int device_scratch(Scratch** out) {
+int Scratch::init() {
+    HEC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    return HEC_OK;
+}
+
+int lease_scratch(Lease<Scratch>& out) {
     int dev;
     int rc = current_device(&dev);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(g_scratch_mu);
-    auto it = g_scratch.find(dev);
-    if (it == g_scratch.end()) {
-        std::unique_ptr<Scratch> sc(new Scratch());
-        HEC_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
-        it = g_scratch.emplace(dev, std::move(sc)).first;
+    SlotPool<Scratch>* pool;
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        std::unique_ptr<SlotPool<Scratch>>& p = g_scratch[dev];
+        if (!p) p.reset(new SlotPool<Scratch>());
+        pool = p.get();
     }
-    *out = it->second.get();
-    return HEC_OK;
+    return pool->lease(out);
 }
 
 static uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -479,9 +483,9 @@ static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* co
     GeomDevice* gd;
     int rc = geom_device(rs, &gd);
     if (rc) return rc;
-    Scratch* sc;
-    if ((rc = device_scratch(&sc))) return rc;
-    std::lock_guard<std::mutex> lk(sc->mu);
+    Lease<Scratch> lease;
+    if ((rc = lease_scratch(lease))) return rc;
+    Scratch* sc = lease.sc;
     const uint64_t Lp = round_up(L, 256);
     if ((rc = sc->reserve(size_t(Lp) * rs->n))) return rc;
     uint8_t* par = sc->dbuf + size_t(rs->k) * Lp;
@@ -557,9 +561,9 @@ static int reconstruct_host(const hec_rs* rs, uint8_t* const* shards, const size
     for (uint32_t id : out_ids)
         if (!shards[id]) return fail(HEC_ERR_INVALID_ARGUMENT, "missing shard without a buffer");
     if (noop) return HEC_OK;
-    Scratch* sc;
-    if ((rc = device_scratch(&sc))) return rc;
-    std::lock_guard<std::mutex> lk(sc->mu);
+    Lease<Scratch> lease;
+    if ((rc = lease_scratch(lease))) return rc;
+    Scratch* sc = lease.sc;
     const uint64_t Lp = round_up(L, 256);
     if ((rc = sc->reserve(size_t(Lp) * rs->n))) return rc;
     HostPlans hp;

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -141,10 +142,55 @@ struct Scratch {
     size_t hcap = 0;
     DevicePlanSet adhoc;
     Completion done;
+    int init();
     int reserve(size_t bytes);
     int reserve_host(size_t bytes);
 };
-int device_scratch(Scratch** out);
+// Scratch slots per device: a host call leases one (its own stream, staging
+// buffers and completion flag), so concurrent calls from several threads
+// overlap on the GPU instead of queueing behind one mutex (SURVEY.md §8b:
+// reentrant, a stream per call). Free slots are taken first; a new slot is
+// created while fewer than kScratchSlots exist; past that a call waits for
+// one. The lease holds the slot's mutex until it is destroyed.
+constexpr int kScratchSlots = 8;
+template <typename S>
+struct Lease {
+    S* sc = nullptr;
+    std::unique_lock<std::mutex> lk;
+};
+// Per-device pool of S (S has `std::mutex mu` and `int init()`, called once
+// when a slot is created).
+template <typename S>
+struct SlotPool {
+    std::mutex mu;
+    std::vector<std::unique_ptr<S>> slots;
+    unsigned rr = 0;
+    int lease(Lease<S>& out) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            for (auto& sl : slots) {
+                std::unique_lock<std::mutex> l(sl->mu, std::try_to_lock);
+                if (l.owns_lock()) {
+                    out.sc = sl.get();
+                    out.lk = std::move(l);
+                    return 0;
+                }
+            }
+            if (slots.size() < size_t(kScratchSlots)) {
+                std::unique_ptr<S> s(new S());
+                if (int rc = s->init()) return rc;
+                out.lk = std::unique_lock<std::mutex>(s->mu);
+                out.sc = s.get();
+                slots.push_back(std::move(s));
+                return 0;
+            }
+            out.sc = slots[rr++ % slots.size()].get();
+        }
+        out.lk = std::unique_lock<std::mutex>(out.sc->mu);  // every slot busy: wait for one
+        return 0;
+    }
+};
+int lease_scratch(Lease<Scratch>& out);
 
 // Zero-copy switch (hec_set_host_zero_copy): pinned host memory the GPU can
 // address is coded by the kernels in place over PCIe instead of being copied.

@@ -55,14 +55,17 @@ struct RaggedScratch {
     uint8_t* hmeta = nullptr;
     uint8_t* dmeta = nullptr;
     size_t mcap = 0;
+    int init() {
+        HEC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        return HEC_OK;
+    }
     int reserve(size_t bytes, size_t meta) {
-        if (!stream) HEC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         if (bytes > cap && bytes > 0) {
             if (host) HEC_HIP(hipHostFree(host));
             if (dev) HEC_HIP(hipFree(dev));
             host = dev = nullptr;
             cap = 0;
-            const size_t want = std::max(bytes, size_t(64) << 20);
+            const size_t want = std::max(bytes, size_t(16) << 20);
             HEC_TRY(pinned_alloc(reinterpret_cast<void**>(&host), want));
             HEC_HIP(hipMalloc(reinterpret_cast<void**>(&dev), want));
             cap = want;
@@ -81,17 +84,21 @@ struct RaggedScratch {
     }
 };
 
-int ragged_scratch(RaggedScratch** out) {
+// Per-device pool of ragged scratch slots (see SlotPool, hec_internal.hpp).
+int lease_ragged(Lease<RaggedScratch>& out) {
     static std::mutex mu;
-    static std::map<int, RaggedScratch*>* reg = new std::map<int, RaggedScratch*>();  // process lifetime
+    static auto* reg = new std::map<int, std::unique_ptr<SlotPool<RaggedScratch>>>();  // process lifetime
     int dev;
     int rc = current_device(&dev);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(mu);
-    auto& p = (*reg)[dev];
-    if (!p) p = new RaggedScratch();
-    *out = p;
-    return HEC_OK;
+    SlotPool<RaggedScratch>* pool;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto& p = (*reg)[dev];
+        if (!p) p.reset(new SlotPool<RaggedScratch>());
+        pool = p.get();
+    }
+    return pool->lease(out);
 }
 
 }  // namespace
@@ -120,9 +127,9 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     GeomDevice* gd;
     int rc = geom_device(rs, &gd);
     if (rc) return rc;
-    RaggedScratch* sc;
-    if ((rc = ragged_scratch(&sc))) return rc;
-    std::lock_guard<std::mutex> lk(sc->mu);
+    Lease<RaggedScratch> lease;
+    if ((rc = lease_ragged(lease))) return rc;
+    RaggedScratch* sc = lease.sc;
     std::vector<RaggedItem> items(jobs.size());
     std::vector<uint32_t> block_item;
     for (size_t j = 0; j < jobs.size(); ++j) {
@@ -317,15 +324,14 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     GeomDevice* gd;
     int rc = geom_device(rs, &gd);
     if (rc) return rc;
-    RaggedScratch* sc;
-    if ((rc = ragged_scratch(&sc))) return rc;
-    std::lock_guard<std::mutex> lk(sc->mu);
+    Lease<RaggedScratch> lease;
+    if ((rc = lease_ragged(lease))) return rc;
+    RaggedScratch* sc = lease.sc;
     const size_t items_bytes = size_t(n) * sizeof(RaggedItem);
     const size_t map_off = (items_bytes + 255) / 256 * 256;
     const size_t meta = map_off + n_blocks * 4;
     MetaSlot& slot = sc->slots[sc->next_slot++ % kMetaSlots];
     if ((rc = slot.reserve(meta))) return rc;  // waits for this slot's previous kernel only
-    if (!sc->stream) HEC_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     if (decode && (rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
     // items and workgroup map written straight into the pinned slot
     RaggedItem* items = reinterpret_cast<RaggedItem*>(slot.h);

@@ -431,6 +431,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--shard-len", type=int, default=1 << 20)
+    ap.add_argument("--shard-pad", type=int, default=64 << 10,
+                    help="HBM layout: shard stride = shard_len + this (DESIGN.md 'Data layout in HBM')")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the end-to-end and mixed-workload sections")
@@ -525,8 +527,8 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
 
     S, L = args.stripes, args.shard_len
     rs = H.ReedSolomon(K_DATA, M_PARITY)
-    t = torch.empty((S, N_TOTAL, L), dtype=torch.uint8, device="cuda")
-    B.fill_splitmix(t, K_DATA * L, rank_seed_base(rank))
+    t = B.empty_stripes(S, N_TOTAL, L, shard_pad=args.shard_pad)
+    B.fill_stripes_splitmix(t, K_DATA, rank_seed_base(rank))  # same bytes as a packed batch
     masks = torch.from_numpy(erasure_masks(S, rank)).cuda()
     stream = torch.cuda.current_stream()
 
@@ -574,6 +576,7 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
         from oracle import corc
         ref = corc.encode_stripes(t[0:2, :K_DATA].cpu().numpy().copy())
         chk_ok &= bool(np.array_equal(t[0:2, K_DATA:].cpu().numpy(), ref))
+    t_shard_stride = t.stride(1)
     del t
     # every rank's verification counts: the job is verified only if all are
     chk_ok = reduce_max(0.0 if chk_ok else 1.0, world) == 0.0
@@ -646,6 +649,7 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
             "config": {"workload": f"RS(10,4) encode + 4-erasure decode, {S} stripes x {L} B shards per GPU "
                                    f"(BASELINE configs 2+3), device-resident",
                        "stripes_per_gpu": S, "shard_len": L, "erasures_per_stripe": 4,
+                       "shard_stride": t_shard_stride,
                        "parallelism": f"independent stripe batches x{world}"},
             # the dominant kernel: the launch with the larger share of the step
             "roofline": dominant,

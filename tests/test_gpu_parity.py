@@ -959,3 +959,38 @@ def test_randomised_ragged_batches_vs_oracle(gpu):
                 continue
             for i in range(14):
                 assert np.array_equal(got[o + i * st: o + i * st + L], want[j][i]), (case, j, i, "decode")
+
+
+@pytest.mark.parametrize("L,pad", [(4096, 65536), (65536, 8), (1 << 20, 64 << 10)])
+def test_padded_batch_layout(gpu, L, pad):
+    """The bench's HBM layout (batch.empty_stripes: shard stride L + pad):
+    fill_stripes_splitmix writes the same data bytes as the packed fill, and
+    encode + a per-stripe 4-erasure rebuild on the padded batch match the C
+    oracle; the pad bytes between shards are never written."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    S = 5
+    rs = H.ReedSolomon(10, 4)
+    t = B.empty_stripes(S, 14, L, shard_pad=pad)
+    assert t.stride() == (14 * (L + pad), L + pad, 1)
+    raw = t.as_strided((t.untyped_storage().nbytes(),), (1,), 0)
+    raw.fill_(0xA5)
+    B.fill_stripes_splitmix(t, 10, O.STRIPE_SEED_BASE)
+    packed = _stripes(S, L)
+    assert torch.equal(t[:, :10], packed[:, :10])
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
+    full = host.copy()
+    drops = [(s % 14, (s + 3) % 14, (s + 7) % 14, (s + 11) % 14) for s in range(S)]
+    masks = torch.tensor([0x3FFF & ~sum(1 << i for i in d) for d in drops], dtype=torch.int32, device="cuda")
+    for s, d in enumerate(drops):
+        for i in d:
+            t[s, i] = 0
+    B.reconstruct_batch(rs, t, masks)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), full)
+    gaps = raw.view(S * 14, L + pad)[:, L:]
+    assert bool((gaps == 0xA5).all())

@@ -1,6 +1,7 @@
 // The BASELINE device-resident workload driven through the C ABI alone
 // (include/hec.h), as a C/Rust consumer would call it: no Python, no PyTorch.
-// Per worker: S x [14][1 MiB] stripes in HBM, splitmix64 data
+// Per worker: S x [14][1 MiB] stripes in HBM (a 64 KiB gap after every shard,
+// as bench.py lays its batch out; argv[5] sets the gap), splitmix64 data
 // (hec_gpu_fill_splitmix), encode (hec_gpu_encode_batch) then a 4-erasure
 // reconstruct (hec_gpu_reconstruct_batch), timed with HIP events on the
 // worker's own stream. Checks: sampled stripes are erased on the device and
@@ -11,7 +12,7 @@
 // scaling. Workers start together after a host barrier; the job time is the
 // slowest worker's wall time over the timed steps.
 //
-//   make build/cabi_bench && build/cabi_bench [stripes] [steps] [warmup] [workers]
+//   make build/cabi_bench && build/cabi_bench [stripes] [steps] [warmup] [workers] [shard_gap]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,7 +48,9 @@
 
 namespace {
 
-constexpr uint64_t L = 1ull << 20, N = HEC_TOTAL_SHARDS_COUNT, kStripe = N * L;
+constexpr uint64_t L = 1ull << 20, N = HEC_TOTAL_SHARDS_COUNT;
+uint64_t P = L + (64ull << 10);  // shard stride
+uint64_t kStripe = N * P;        // stripe stride
 
 uint64_t splitmix(uint64_t& s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -102,7 +105,11 @@ int worker(int t, int device, uint32_t S, int steps, int warmup, hec_rs_t* rs, B
     HIPCHECK(hipMalloc(&d_masks, S * 4));
     HIPCHECK(hipMalloc(&d_bad, 4));
     // worker t's stripes are seeded like bench.py's rank t
-    HECCHECK(hec_gpu_fill_splitmix(d, kStripe, HEC_DATA_SHARDS_COUNT * L, S, 0x5EED0000ull + (uint64_t(t) << 20), st));
+    // shard i holds words i * L / 8 on of its stripe's splitmix64 stream: the
+    // bytes a packed batch gets from one hec_gpu_fill_splitmix per stripe
+    for (uint64_t i = 0; i < HEC_DATA_SHARDS_COUNT; ++i)
+        HECCHECK(hec_gpu_fill_splitmix(d + i * P, kStripe, L, S,
+                                       0x5EED0000ull + (uint64_t(t) << 20) + i * (L / 8) * 0x9E3779B97F4A7C15ull, st));
 
     // 4 erasures per stripe, uniform over the 1001 patterns (seeded per worker)
     std::vector<uint32_t> masks(S);
@@ -117,9 +124,9 @@ int worker(int t, int device, uint32_t S, int steps, int warmup, hec_rs_t* rs, B
     HIPCHECK(hipMemsetAsync(d_bad, 0, 4, st));
 
     auto encode = [&] {
-        return hec_gpu_encode_batch(rs, d, kStripe, L, d + HEC_DATA_SHARDS_COUNT * L, kStripe, L, L, S, st);
+        return hec_gpu_encode_batch(rs, d, kStripe, P, d + HEC_DATA_SHARDS_COUNT * P, kStripe, P, L, S, st);
     };
-    auto decode = [&] { return hec_gpu_reconstruct_batch(rs, d, kStripe, L, L, S, d_masks, d_bad, st); };
+    auto decode = [&] { return hec_gpu_reconstruct_batch(rs, d, kStripe, P, L, S, d_masks, d_bad, st); };
     for (int i = 0; i < warmup; ++i) {
         HECCHECK(encode());
         HECCHECK(decode());
@@ -154,8 +161,8 @@ int worker(int t, int device, uint32_t S, int steps, int warmup, hec_rs_t* rs, B
     HIPCHECK(hipMemcpy(want.data(), d, V * kStripe, hipMemcpyDeviceToHost));
     for (uint32_t s = 0; s < V; ++s)
         for (uint64_t i = 0; i < N; ++i)
-            if (!((masks[s] >> i) & 1)) HIPCHECK(hipMemsetAsync(d + s * kStripe + i * L, 0xA5, L, st));
-    HECCHECK(hec_gpu_reconstruct_batch(rs, d, kStripe, L, L, V, d_masks, d_bad, st));
+            if (!((masks[s] >> i) & 1)) HIPCHECK(hipMemsetAsync(d + s * kStripe + i * P, 0xA5, L, st));
+    HECCHECK(hec_gpu_reconstruct_batch(rs, d, kStripe, P, L, V, d_masks, d_bad, st));
     HIPCHECK(hipStreamSynchronize(st));
     HIPCHECK(hipMemcpy(got.data(), d, V * kStripe, hipMemcpyDeviceToHost));
     uint32_t bad = 0;
@@ -178,7 +185,10 @@ int main(int argc, char** argv) {
     const int steps = argc > 2 ? std::atoi(argv[2]) : 10;
     const int warmup = argc > 3 ? std::atoi(argv[3]) : 3;
     const int workers = argc > 4 ? std::atoi(argv[4]) : 1;
-    if (S == 0 || steps <= 0 || warmup < 0 || workers <= 0 || workers > 64) return 1;
+    const long gap = argc > 5 ? std::atol(argv[5]) : 64l << 10;
+    if (S == 0 || steps <= 0 || warmup < 0 || workers <= 0 || workers > 64 || gap < 0) return 1;
+    P = L + uint64_t(gap);
+    kStripe = N * P;
     int count = 0;
     HECCHECK(hec_device_count(&count));
     hec_rs_t* rs = nullptr;  // one immutable context shared by every worker (hec.h threading rules)
@@ -202,14 +212,14 @@ int main(int argc, char** argv) {
         dec = std::max(dec, res[t].dec_ms);
         devs += (t ? "," : "") + std::to_string(res[t].device);
     }
-    const double bytes = double(S) * kStripe;  // per worker and launch: encode 10 L + 4 L, decode 10 + 4
+    const double bytes = double(S) * N * L;  // per worker and launch: encode 10 L + 4 L, decode 10 + 4
     const double payload = 2.0 * workers * S * HEC_DATA_SHARDS_COUNT * L * steps;
     std::printf("{\"tool\": \"cabi_bench\", \"api\": \"hec_gpu_encode_batch + hec_gpu_reconstruct_batch\", "
                 "\"workers\": %d, \"devices\": [%s], \"visible_devices\": %d, \"stripes_per_worker\": %u, "
-                "\"shard_len\": %llu, \"steps\": %d, \"job_data_GiB_s\": %.1f, \"encode_ms\": %.4f, "
+                "\"shard_len\": %llu, \"shard_stride\": %llu, \"steps\": %d, \"job_data_GiB_s\": %.1f, \"encode_ms\": %.4f, "
                 "\"decode_ms\": %.4f, \"encode_TBps\": %.3f, \"decode_TBps\": %.3f, \"encode_frac\": %.4f, "
                 "\"encode_kernel\": \"%s\", \"verified\": %s}\n",
-                workers, devs.c_str(), count, S, (unsigned long long)L, steps, payload / wall / double(1ull << 30),
+                workers, devs.c_str(), count, S, (unsigned long long)L, (unsigned long long)P, steps, payload / wall / double(1ull << 30),
                 enc, dec, bytes / enc / 1e9, bytes / dec / 1e9, bytes / enc / 1e9 / 8.0, hec_encode_kernel_name(L),
                 ok ? "true" : "false");
     return ok ? 0 : 3;

@@ -5,7 +5,10 @@ GiB/s per round and the per-launch split (HIP events) so host gaps between
 launches show up: gap = wall per rep - encode - reconstruct. HEC_LIB_PATH
 selects a measurement build.
 
-python tools/mixed_probe.py [--rounds 5] [--reps 5]
+python tools/mixed_probe.py [--rounds 5] [--reps 5] [--pads 0,65536]
+
+--pads: shard gaps compared inside ONE allocation (the layouts take turns
+each round), as tools/layout_in_alloc_probe.py does for the bench batch.
 """
 import argparse
 import json
@@ -29,6 +32,7 @@ def main():
     ap.add_argument("--uniform", type=int, default=0,
                     help="E > 0: every stripe 1 MiB with exactly E random erasures (the bench batch through "
                          "the ragged kernels; compare with the strided kernels' times)")
+    ap.add_argument("--pads", default="0", help="gap after every shard, one layout per value")
     args = ap.parse_args()
     import torch
     import helyim_amd as H
@@ -45,37 +49,50 @@ def main():
         es = np.full(n, args.uniform)
     full = (1 << 14) - 1
     masks = [full & ~int(sum(1 << int(i) for i in rng.choice(14, int(e), replace=False))) for e in es]
-    descs, off = [], 0
-    for s in range(n):
-        descs.append((off, int(Ls[s]), int(Ls[s]), int(masks[s])))
-        off += 14 * int(Ls[s])
-    dev = torch.empty(off, dtype=torch.uint8, device="cuda")
-    for s, (o, st, L, _) in enumerate(descs):
-        B.fill_splitmix(dev[o:o + 10 * L].view(1, 1, -1), 10 * L, bench.rank_seed_base(0) + s)
+    pads = [int(x) for x in args.pads.split(",")]
+
+    def layout(pad):
+        descs, off = [], 0
+        for s in range(n):
+            descs.append((off, int(Ls[s]) + pad, int(Ls[s]), int(masks[s])))
+            off += 14 * (int(Ls[s]) + pad)
+        return descs, off
+
+    lays = {p: layout(p) for p in pads}
+    dev = torch.empty(max(o for _, o in lays.values()), dtype=torch.uint8, device="cuda")
+    for s, (o, st, L, _) in enumerate(lays[pads[0]][0]):
+        for i in range(10):
+            B.fill_splitmix(dev[o + i * st:o + i * st + L].view(1, 1, -1), L, bench.rank_seed_base(0) + 14 * s + i)
+    descs = lays[pads[0]][0]
     payload = sum(10 * d[2] for d in descs) + sum(10 * d[2] for d in descs if d[3] != full)
-    B.encode_ragged(rs, dev, descs)
-    B.reconstruct_ragged(rs, dev, descs)
+    for p in pads:
+        B.encode_ragged(rs, dev, lays[p][0])
+        B.reconstruct_ragged(rs, dev, lays[p][0])
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     for r in range(args.rounds):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
-        ev[0].record(st)
-        for i in range(args.reps):
-            B.encode_ragged(rs, dev, descs)
-            ev[2 * i + 1].record(st)
-            B.reconstruct_ragged(rs, dev, descs)
-            ev[2 * i + 2].record(st)
-        torch.cuda.synchronize()
-        enc = np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)])
-        dec = np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)])
-        wall = ev[0].elapsed_time(ev[-1]) / args.reps
-        enc_b = sum(14 * d[2] for d in descs)
-        dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
-        print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n, "round": r,
-                          "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
-                          "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
-                          "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3), "dec_ms": round(float(dec), 3),
-                          "payload_GiB": round(payload / 2**30, 3)}), flush=True)
+        for p in pads:
+            descs = lays[p][0]
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
+            ev[0].record(st)
+            for i in range(args.reps):
+                B.encode_ragged(rs, dev, descs)
+                ev[2 * i + 1].record(st)
+                B.reconstruct_ragged(rs, dev, descs)
+                ev[2 * i + 2].record(st)
+            torch.cuda.synchronize()
+            enc = np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)])
+            dec = np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)])
+            wall = ev[0].elapsed_time(ev[-1]) / args.reps
+            enc_b = sum(14 * d[2] for d in descs)
+            dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
+            print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
+                              "pad": p, "round": r,
+                              "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
+                              "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
+                              "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),
+                              "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3)}), flush=True)
+    descs = lays[pads[0]][0]
     if args.grouped:
         del dev
         grouped(rs, B, torch, Ls, masks, args.rounds, args.reps)

@@ -32,7 +32,8 @@ def main():
     ap.add_argument("--encs", default="0", help="encode kernel: 0 table lookup, 1 bit-sliced")
     ap.add_argument("--decvecs", default="8", help="decode bytes per lane (8 default, 16, 4)")
     ap.add_argument("--encvecs", default="16", help="table-encode bytes per lane (16 default, 8, 4)")
-    ap.add_argument("--pad", type=int, default=0, help="extra bytes between shards (breaks 2^20 strides)")
+    ap.add_argument("--pad", type=int, default=64 << 10,
+                    help="extra bytes between shards (default: the bench's batch.SHARD_PAD)")
     ap.add_argument("--stripe-pad", type=int, default=0, help="extra bytes between stripes (shards stay 1 MiB apart)")
     ap.add_argument("--tile", type=int, default=0,
                     help="interleaved layout: every shard split in tiles of this many bytes, the 14 "
@@ -52,8 +53,8 @@ def main():
     if args.stripe_pad:
         t = torch.empty((S, 14 * L + args.stripe_pad), dtype=torch.uint8, device="cuda")[:, :14 * L].view(S, 14, L)
     else:
-        t = torch.empty((S, 14, L + args.pad), dtype=torch.uint8, device="cuda")[:, :, :L]
-    B.fill_splitmix(t, 10 * L, 0x5EED0000)
+        t = B.empty_stripes(S, 14, L, shard_pad=args.pad)
+    B.fill_stripes_splitmix(t, 10, 0x5EED0000)
     masks = torch.from_numpy(mask_np).cuda()
     B.encode_batch(rs, t)
     torch.cuda.synchronize()
@@ -104,10 +105,10 @@ def main():
                           "dec_ms_med": round(float(np.median(dec)), 3),
                           "dec_GBps": round(nbytes / np.median(dec) / 1e6, 1)}), flush=True)
     # the XOR-only rows scribbled over data shards through decode: regenerate
-    B.fill_splitmix(t, 10 * L, 0x5EED0000)
+    B.fill_stripes_splitmix(t, 10, 0x5EED0000)
     B.encode_batch(rs, t)
     torch.cuda.synchronize()
-    if not args.pad and not args.stripe_pad:
+    if not args.stripe_pad:
         assert torch.equal(t[:8], good)
 
 

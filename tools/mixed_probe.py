@@ -33,6 +33,7 @@ def main():
                     help="E > 0: every stripe 1 MiB with exactly E random erasures (the bench batch through "
                          "the ragged kernels; compare with the strided kernels' times)")
     ap.add_argument("--pads", default="0", help="gap after every shard, one layout per value")
+    ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes), per round")
     args = ap.parse_args()
     import torch
     import helyim_amd as H
@@ -70,28 +71,29 @@ def main():
         B.reconstruct_ragged(rs, dev, lays[p][0])
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
-    for r in range(args.rounds):
-        for p in pads:
-            descs = lays[p][0]
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
-            ev[0].record(st)
-            for i in range(args.reps):
-                B.encode_ragged(rs, dev, descs)
-                ev[2 * i + 1].record(st)
-                B.reconstruct_ragged(rs, dev, descs)
-                ev[2 * i + 2].record(st)
-            torch.cuda.synchronize()
-            enc = np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)])
-            dec = np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)])
-            wall = ev[0].elapsed_time(ev[-1]) / args.reps
-            enc_b = sum(14 * d[2] for d in descs)
-            dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
-            print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
-                              "pad": p, "round": r,
-                              "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
-                              "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
-                              "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),
-                              "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3)}), flush=True)
+    for r, p, dv in ((r, p, int(dv)) for r in range(args.rounds) for p in pads for dv in args.decvecs.split(",")):
+        H.lib.hec_set_decode_vector_bytes(dv)
+        descs = lays[p][0]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
+        ev[0].record(st)
+        for i in range(args.reps):
+            B.encode_ragged(rs, dev, descs)
+            ev[2 * i + 1].record(st)
+            B.reconstruct_ragged(rs, dev, descs)
+            ev[2 * i + 2].record(st)
+        torch.cuda.synchronize()
+        enc = np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)])
+        dec = np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)])
+        wall = ev[0].elapsed_time(ev[-1]) / args.reps
+        enc_b = sum(14 * d[2] for d in descs)
+        dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
+        print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
+                          "pad": p, "dec_vec_bytes": dv, "round": r,
+                          "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
+                          "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
+                          "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),
+                          "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3)}), flush=True)
+    H.lib.hec_set_decode_vector_bytes(8)
     descs = lays[pads[0]][0]
     if args.grouped:
         del dev

@@ -207,6 +207,16 @@ def empty_stripes(n_stripes: int, total: int, shard_len: int, shard_pad: int = S
     return buf.as_strided((n_stripes, total, shard_len), (total * shard, shard, 1))
 
 
+def shard_seed(seed_base: int, shard: int, shard_len: int) -> int:
+    """Seed under which hec_gpu_fill_splitmix writes shard ``shard`` of a
+    stripe seeded ``seed_base`` on its own: word n of the stripe stream is
+    mix(seed + (n + 1) * gamma), so the stream from word shard * L / 8 on is
+    the stream of seed + shard * (L / 8) * gamma (L a multiple of 8)."""
+    if shard_len % 8:
+        raise ValueError("shard_len must be a multiple of 8")
+    return (seed_base + shard * (shard_len // 8) * _GOLDEN) & ((1 << 64) - 1)
+
+
 def fill_stripes_splitmix(t: torch.Tensor, data_shards: int, seed_base: int, stream=None) -> None:
     """The data shards of ``t[S, total, L]`` get exactly the bytes
     ``fill_splitmix`` writes into a packed batch (stripe s = one splitmix64
@@ -222,7 +232,7 @@ def fill_stripes_splitmix(t: torch.Tensor, data_shards: int, seed_base: int, str
     if L % 8:
         raise ValueError("a padded batch needs shard_len % 8 == 0 (the generator emits 8-byte words)")
     for i in range(data_shards):
-        fill_splitmix(t[:, i], L, (seed_base + i * (L // 8) * _GOLDEN) & ((1 << 64) - 1), stream)
+        fill_splitmix(t[:, i], L, shard_seed(seed_base, i, L), stream)
 
 
 def set_launch_config(vec_per_thread: int = 1, max_blocks: int = 0, xcd_remap: int = 1,

@@ -72,6 +72,21 @@ def test_splitmix_py_vs_c():
         assert np.array_equal(O.splitmix64_bytes(seed, n), corc.splitmix64_bytes(seed, n))
 
 
+@pytest.mark.parametrize("L", [8, 4096, 65536, 1 << 20])
+def test_shard_seed_splits_the_stripe_stream(L):
+    """batch.shard_seed (the padded batch fill, bench.py's layout): shard i
+    filled on its own under shard_seed(seed, i, L) holds the bytes of the
+    stripe's one splitmix64 stream at [i * L, (i + 1) * L); seeds near 2^64
+    wrap as the C generator's uint64 arithmetic does."""
+    from helyim_amd.batch import shard_seed
+    for seed in (0x5EED0000, 0x5EED0000 + (3 << 20) + 17, (1 << 64) - 5):
+        stream = corc.splitmix64_bytes(seed, 10 * L)
+        for i in range(10):
+            assert np.array_equal(corc.splitmix64_bytes(shard_seed(seed, i, L), L), stream[i * L:(i + 1) * L]), (seed, i)
+    with pytest.raises(ValueError):
+        shard_seed(1, 1, 12)
+
+
 def test_encode_vectors_fixture(golden):
     g = golden("encode_vectors.json")
     rs = O.ReedSolomon(10, 4)

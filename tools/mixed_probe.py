@@ -34,6 +34,8 @@ def main():
                          "the ragged kernels; compare with the strided kernels' times)")
     ap.add_argument("--pads", default="0", help="gap after every shard, one layout per value")
     ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes), per round")
+    ap.add_argument("--strided", action="store_true",
+                    help="with --uniform: also time the strided kernels on the same bytes each round")
     args = ap.parse_args()
     import torch
     import helyim_amd as H
@@ -71,15 +73,26 @@ def main():
         B.reconstruct_ragged(rs, dev, lays[p][0])
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
-    for r, p, dv in ((r, p, int(dv)) for r in range(args.rounds) for p in pads for dv in args.decvecs.split(",")):
+    kinds = ["ragged"] + (["strided"] if args.strided and args.uniform else [])
+    mask_t = torch.tensor(masks, dtype=torch.int32, device="cuda")
+    for r, p, dv, kind in ((r, p, int(dv), k) for r in range(args.rounds) for p in pads
+                           for dv in args.decvecs.split(",") for k in kinds):
         H.lib.hec_set_decode_vector_bytes(dv)
         descs = lays[p][0]
+        L0 = int(Ls[0])
+        view = dev.as_strided((n, 14, L0), (14 * (L0 + p), L0 + p, 1))
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
         ev[0].record(st)
         for i in range(args.reps):
-            B.encode_ragged(rs, dev, descs)
+            if kind == "ragged":
+                B.encode_ragged(rs, dev, descs)
+            else:
+                B.encode_batch(rs, view)
             ev[2 * i + 1].record(st)
-            B.reconstruct_ragged(rs, dev, descs)
+            if kind == "ragged":
+                B.reconstruct_ragged(rs, dev, descs)
+            else:
+                B.reconstruct_batch(rs, view, mask_t)
             ev[2 * i + 2].record(st)
         torch.cuda.synchronize()
         enc = np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)])
@@ -88,7 +101,7 @@ def main():
         enc_b = sum(14 * d[2] for d in descs)
         dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
-                          "pad": p, "dec_vec_bytes": dv, "round": r,
+                          "kind": kind, "pad": p, "dec_vec_bytes": dv, "round": r,
                           "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
                           "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),

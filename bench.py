@@ -362,16 +362,19 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
     data = int(sum(K_DATA * d[2] for d in descs))
     # decode payload counts only stripes with an erasure (e = 0 is upstream's no-op)
     dec_data = int(sum(K_DATA * d[2] for d in descs if d[3] != full))
-    B.encode_ragged(rs, dev, descs)  # warm-up
-    B.reconstruct_ragged(rs, dev, descs)
+    # the descriptors as the C ABI's hec_stripe_desc array, built once (a list
+    # is converted on every call, on the host, with the GPU idle the first time)
+    darr = np.array(descs, dtype=B.desc_dtype())
+    B.encode_ragged(rs, dev, darr)  # warm-up
+    B.reconstruct_ragged(rs, dev, darr)
     torch.cuda.synchronize()
     s_ = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 5
     e0.record(s_)
     for _ in range(reps):
-        B.encode_ragged(rs, dev, descs)
-        B.reconstruct_ragged(rs, dev, descs)
+        B.encode_ragged(rs, dev, darr)
+        B.reconstruct_ragged(rs, dev, darr)
     e1.record(s_)
     torch.cuda.synchronize()
     t_dev = e0.elapsed_time(e1) * 1e-3 / reps

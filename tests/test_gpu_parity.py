@@ -464,15 +464,23 @@ def test_batch_reconstruct_too_few_present(gpu):
     assert np.array_equal(t[0, 10:].cpu().numpy(), ref[0])
 
 
-def test_full_config_roundtrip(gpu):
-    """BASELINE config 2/3 sizes (4096 x 1 MiB): encode -> erase 4 random shards
-    per stripe -> reconstruct == original; sampled stripes vs the C oracle."""
+@pytest.mark.parametrize("pad", [0, 64 << 10])
+def test_full_config_roundtrip(gpu, pad):
+    """BASELINE config 2/3 sizes (4096 x 1 MiB), packed and in the bench's
+    padded layout (a 64 KiB gap after every shard): encode -> erase 4 random
+    shards per stripe -> reconstruct == original; sampled stripes vs the C
+    oracle; the parity checksum survives the round trip."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rs = H.ReedSolomon(10, 4)
     S, L = 4096, 1 << 20
-    t = _stripes(S, L)
+    torch.cuda.empty_cache()
+    if pad:
+        t = B.empty_stripes(S, 14, L, shard_pad=pad)
+        B.fill_stripes_splitmix(t, 10, O.STRIPE_SEED_BASE)
+    else:
+        t = _stripes(S, L)
     B.encode_batch(rs, t)
     torch.cuda.synchronize()
     rng = np.random.default_rng(3)
@@ -493,6 +501,8 @@ def test_full_config_roundtrip(gpu):
     torch.cuda.synchronize()
     assert torch.equal(t[er], snap)
     assert t[:, 10:].view(torch.int64).sum(dtype=torch.int64).item() == parity_sum
+    del t, snap, er
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("lengths", ["odd", "multiple_of_8k"])

@@ -106,7 +106,8 @@ def main():
                           "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
                           "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),
-                          "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3)}), flush=True)
+                          "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3),
+                          "enc_bytes": int(enc_b), "dec_bytes": int(dec_b)}), flush=True)
     H.lib.hec_set_decode_vector_bytes(8)
     descs = lays[pads[0]][0]
     if args.grouped:

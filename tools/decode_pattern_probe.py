@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--shard-len", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--vecs", default="1", help="16-byte vectors per lane (hec_set_launch_config)")
+    ap.add_argument("--modes", default="0", help="0 = GF decode, 1 = its XOR-only twin (same traffic)")
+    ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes)")
+    ap.add_argument("--pad", type=int, default=64 << 10, help="gap after every shard (batch.empty_stripes)")
     args = ap.parse_args()
     import torch
     import helyim_amd as H
@@ -32,8 +35,8 @@ def main():
     import bench
     S, L = args.stripes, args.shard_len
     rs = H.ReedSolomon(10, 4)
-    t = torch.empty((S, 14, L), dtype=torch.uint8, device="cuda")
-    B.fill_splitmix(t, 10 * L, 0x5EED0000)
+    t = B.empty_stripes(S, 14, L, shard_pad=args.pad)
+    B.fill_stripes_splitmix(t, 10, 0x5EED0000)
     B.encode_batch(rs, t)
     full = (1 << 14) - 1
 
@@ -48,7 +51,8 @@ def main():
         pats[f"random{e}"] = np.array([full & ~int(sum(1 << int(i) for i in rng.choice(14, e, replace=False)))
                                        for _ in range(S)], np.int32)
     masks = {k: torch.from_numpy(v).cuda() for k, v in pats.items()}
-    decs = [int(x) for x in args.vecs.split(",")]
+    decs = [(int(v), int(m), int(dv)) for v in args.vecs.split(",") for m in args.modes.split(",")
+            for dv in args.decvecs.split(",")]
     res = {}
     s = torch.cuda.current_stream()
     for _ in range(args.rounds):
@@ -57,21 +61,26 @@ def main():
         B.encode_batch(rs, t)
         e1.record(s)
         torch.cuda.synchronize()
-        res.setdefault(("encode", -1), []).append(e0.elapsed_time(e1))
+        res.setdefault(("encode", (-1, 0, 0)), []).append(e0.elapsed_time(e1))
         for k, m in masks.items():
             for d in decs:
-                B.set_launch_config(vec_per_thread=d)
+                B.set_launch_config(vec_per_thread=d[0])
+                H.lib.hec_set_kernel_mode(d[1])
+                H.lib.hec_set_decode_vector_bytes(d[2])
                 e0.record(s)
                 B.reconstruct_batch(rs, t, m)
                 e1.record(s)
                 torch.cuda.synchronize()
                 res.setdefault((k, d), []).append(e0.elapsed_time(e1))
     B.set_launch_config()
+    H.lib.hec_set_kernel_mode(0)
+    H.lib.hec_set_decode_vector_bytes(8)
     for (k, d), v in res.items():
         e = {"d0,d9,p10": 3, "one_d4": 1, "random1": 1, "random2": 2, "random3": 3}.get(k, 4)
         nbytes = S * (10 + e) * L if k != "encode" else S * 14 * L
         ms = float(np.median(v))
-        print(json.dumps({"pattern": k, "vec_per_thread": d, "lib": os.path.basename(H.LIB_PATH), "ms_med": round(ms, 3),
+        print(json.dumps({"pattern": k, "vec_per_thread": d[0], "mode": ["gf", "xor_only"][d[1]],
+                          "dec_vec_bytes": d[2], "pad": args.pad, "lib": os.path.basename(H.LIB_PATH), "ms_med": round(ms, 3),
                           "GB_s": round(nbytes / ms / 1e6, 1)}), flush=True)
 
 

@@ -8,7 +8,7 @@
 //               (10R4W == the encode pattern with the math removed)
 // One workgroup (256 lanes x 16 B) per 4 KiB chunk unless noted.
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/membench tools/membench.hip
-// Run:   build/membench [pad]      (prints one JSON line per case)
+// Run:   build/membench [pad|mix]  (prints one JSON line per case)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -182,8 +182,32 @@ static int pad_sweep() {
     return 0;
 }
 
+// Read/write mix on the bench's padded layout (shard stride 1 MiB + 64 KiB,
+// XCD eighths): 10 reads + m writes per stripe, m = 0..4, and 13r1w, 12r2w.
+// Does a mostly-read mix run faster per byte than 10r4w?
+static int mix_sweep() {
+    const uint64_t S = 4096, L = 1ull << 20, N = 14, ss = L + 65536;
+    uint8_t* buf;
+    CHECK(hipMalloc(&buf, S * N * ss));
+    CHECK(hipMemset(buf, 0x5a, S * N * ss));
+    const uint32_t cps = uint32_t(L / 4096), grid = uint32_t(S * cps);
+    char extra[96];
+    snprintf(extra, sizeof extra, ", \"shard_stride\": %llu, \"xcd_remap\": 1", (unsigned long long)ss);
+#define MIX(R, W)                                                                                         \
+    run(#R "r" #W "w", extra, double(S * (R + W) * L), [&] {                                              \
+        hipLaunchKernelGGL((k_nrmw<R, W>), dim3(grid), dim3(256), 0, 0, buf, N * ss, ss, cps, 1);         \
+    })
+    for (int round = 0; round < 2; ++round) {
+        MIX(10, 0); MIX(10, 1); MIX(10, 2); MIX(10, 3); MIX(10, 4); MIX(13, 1); MIX(12, 2); MIX(14, 0); MIX(0, 14);
+    }
+#undef MIX
+    CHECK(hipFree(buf));
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "pad") return pad_sweep();
+    if (argc > 1 && std::string(argv[1]) == "mix") return mix_sweep();
     const uint64_t S = 4096, L = 1ull << 20, N = 14;
     const uint64_t total = S * N * L;  // 56 GiB
     uint8_t* buf;

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--modes", default="0", help="0 = GF decode, 1 = its XOR-only twin (same traffic)")
     ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes)")
     ap.add_argument("--pad", type=int, default=64 << 10, help="gap after every shard (batch.empty_stripes)")
+    ap.add_argument("--only", default="", help="comma list of patterns to run (default: all)")
     args = ap.parse_args()
     import torch
     import helyim_amd as H
@@ -46,8 +47,14 @@ def main():
     pats = {"random4": bench.erasure_masks(S, 0), "p10-13": fixed((10, 11, 12, 13)),
             "d0-3": fixed((0, 1, 2, 3)), "d6-9": fixed((6, 7, 8, 9)), "0,5,10,13": fixed((0, 5, 10, 13)),
             "d0,d9,p10": fixed((0, 9, 10)), "one_d4": fixed((4,))}
+    # the bench's patterns with stripes of one pattern adjacent (table reuse)
+    pats["random4_sorted"] = np.sort(pats["random4"])
+    if args.only:
+        pats = {k: pats[k] for k in args.only.split(",")}
     rng = np.random.default_rng(0xE4)
     for e in (1, 2, 3):  # per-stripe random patterns with exactly e erasures
+        if args.only and f"random{e}" not in args.only.split(","):
+            continue
         pats[f"random{e}"] = np.array([full & ~int(sum(1 << int(i) for i in rng.choice(14, e, replace=False)))
                                        for _ in range(S)], np.int32)
     masks = {k: torch.from_numpy(v).cuda() for k, v in pats.items()}

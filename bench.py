@@ -600,6 +600,8 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
     prof = load_traffic()
+    if prof.get("workload", "").split(",")[0] != f"{S} stripes x {L} B":
+        prof = {}  # the committed counters are of another batch size: no traffic figure for this one
 
     extras = {}
     if not args.no_extras:

@@ -1,0 +1,45 @@
+"""The bench line the driver parses (bench.py at N=1, a small batch): exactly
+one JSON line on stdout carrying the contract's keys, a `value` that follows
+from its own step time, a `roofline` whose fraction follows from its achieved
+rate, a verified run and the CPU baseline beside it."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "verified")
+
+
+@pytest.mark.gpu
+def test_bench_line_contract():
+    S, L, steps = 64, 1 << 20, 3  # 0.9 GiB: larger than the 256 MB Infinity Cache
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stripes", str(S), "--shard-len", str(L),
+                        "--steps", str(steps), "--warmup", "1", "--no-extras", "--cpu-seconds", "0.4"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, p.stdout[-3000:]
+    d = json.loads(lines[0])
+    for k in KEYS:
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == 1
+    assert d["unit"] == "GiB/s" and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["dtype"] == "u8" and d["vs_baseline"] is None
+    assert d["verified"] is True
+    assert d["config"]["stripes_per_gpu"] == S and d["config"]["shard_len"] == L
+    # value = encode + decode data payload over the timed steps
+    payload = 2 * S * 10 * L
+    assert d["value"] == pytest.approx(payload / (d["ms_per_step"] * 1e-3) / 2**30, rel=0.01)
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert 0 < r["achieved"] < r["peak"]
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3)
+    assert r["algorithmic_bytes_per_launch"] == S * 14 * L  # 10 reads + 4 writes per stripe either way
+    assert r["traffic"] is None  # the committed PMC bytes are of the 4096 x 1 MiB batch, not this one
+    cb = d["cpu_baseline"]
+    assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0 and cb["sample"]

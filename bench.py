@@ -298,10 +298,11 @@ def load_traffic() -> dict:
     return {}
 
 
-def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) -> dict:
+def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3, devices=None) -> dict:
     """End-to-end rate from pinned host memory (the path helyim runs): host
     stripes -> H2D -> kernel -> D2H, pipelined over 3 streams. Encode moves
-    10 L H2D + 4 L D2H per stripe; a 4-erasure decode 10 L H2D + 4 L D2H."""
+    10 L H2D + 4 L D2H per stripe; a 4-erasure decode 10 L H2D + 4 L D2H.
+    devices: one call spread over these GPUs (hec_host_*_batch_multi)."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -312,14 +313,14 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) ->
     host.copy_(dev)
     del dev
     masks = erasure_masks(S, rank)
-    B.host_encode_batch(rs, host)  # warm-up (pipeline buffers, tables)
-    B.host_reconstruct_batch(rs, host, masks)
+    B.host_encode_batch(rs, host, devices=devices)  # warm-up (pipeline buffers, tables)
+    B.host_reconstruct_batch(rs, host, masks, devices=devices)
     enc0 = time.time()
     for _ in range(reps):
-        B.host_encode_batch(rs, host)
+        B.host_encode_batch(rs, host, devices=devices)
     enc1 = dec0 = time.time()
     for _ in range(reps):
-        B.host_reconstruct_batch(rs, host, masks)
+        B.host_reconstruct_batch(rs, host, masks, devices=devices)
     dec1 = time.time()
     te, td = (enc1 - enc0) / reps, (dec1 - dec0) / reps
     data = S * K_DATA * L
@@ -327,7 +328,7 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) ->
     del host
     buf.close()
     return {"stripes": S, "shard_len": L, "host_memory": "pinned (hec_host_alloc: this GPU's NUMA node)",
-            "host_numa_node": node,
+            "host_numa_node": node, "devices": devices if devices is not None else "current",
             "raw": {"data_bytes": data * reps, "encode": [enc0, enc1], "decode": [dec0, dec1]},
             "encode_data_GiB_s": round(data / te / 2**30, 2),
             "decode_data_GiB_s": round(data / td / 2**30, 2),
@@ -335,11 +336,14 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3) ->
             "decode_pcie_GB_s": round(S * N_TOTAL * L / td / 1e9, 2)}
 
 
-def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
+def mixed_section(rs, rank: int, n_stripes: int = 2048, e2e_stripes: int = 512) -> dict:
     """BASELINE config 5: shard lengths 64 KiB..4 MiB (log-uniform), 0..4
-    erasures per stripe. Device-resident: all stripes packed in one HBM buffer,
-    one ragged encode launch + one ragged reconstruct launch. End to end: the
-    pinned-host pipeline (hec_host_*_batch), one call per length group."""
+    erasures per stripe. Device-resident: all n_stripes packed in one HBM
+    buffer, one ragged encode launch + one ragged reconstruct launch, each
+    timed with its own HIP events (2048 stripes: the 512-stripe launch lost
+    ~3% to its fixed cost, profiles/r03/sweep_mixed1.jsonl). End to end: the
+    first e2e_stripes stripes through the pinned-host pipeline
+    (hec_host_*_batch), one call per length group."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -362,6 +366,8 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
     data = int(sum(K_DATA * d[2] for d in descs))
     # decode payload counts only stripes with an erasure (e = 0 is upstream's no-op)
     dec_data = int(sum(K_DATA * d[2] for d in descs if d[3] != full))
+    enc_hbm = int(sum(N_TOTAL * d[2] for d in descs))  # algorithmic bytes: read 10 L + write 4 L
+    dec_hbm = int(sum((K_DATA + N_TOTAL - bin(d[3]).count("1")) * d[2] for d in descs if d[3] != full))
     # the descriptors as the C ABI's hec_stripe_desc array, built once (a list
     # is converted on every call, on the host, with the GPU idle the first time)
     darr = np.array(descs, dtype=B.desc_dtype())
@@ -369,18 +375,22 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
     B.reconstruct_ragged(rs, dev, darr)
     torch.cuda.synchronize()
     s_ = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 5
-    e0.record(s_)
-    for _ in range(reps):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps + 1)]
+    ev[0].record(s_)
+    for i in range(reps):
         B.encode_ragged(rs, dev, darr)
+        ev[2 * i + 1].record(s_)
         B.reconstruct_ragged(rs, dev, darr)
-    e1.record(s_)
+        ev[2 * i + 2].record(s_)
     torch.cuda.synchronize()
-    t_dev = e0.elapsed_time(e1) * 1e-3 / reps
+    t_dev = ev[0].elapsed_time(ev[-1]) * 1e-3 / reps
+    enc_ms = float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)]))
+    dec_ms = float(np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(reps)]))
     groups, bufs = [], []
+    sub_idx = range(min(e2e_stripes, n_stripes))
     for L in lens:
-        idx = [s for s in range(n_stripes) if Ls[s] == L]
+        idx = [s for s in sub_idx if Ls[s] == L]
         if not idx:
             continue
         hb = H.HostBuffer(len(idx) * N_TOTAL * L)  # pinned, on this GPU's NUMA node
@@ -391,6 +401,7 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
             h[j].view(-1).copy_(dev[o:o + N_TOTAL * L])
         groups.append((h, masks[idx].astype(np.uint32)))
     del dev
+    e2e_payload = int(sum(K_DATA * descs[s][2] * (2 if descs[s][3] != full else 1) for s in sub_idx))
     for h, m in groups:
         B.host_encode_batch(rs, h)
     w0 = time.time()
@@ -407,8 +418,45 @@ def mixed_section(rs, rank: int, n_stripes: int = 512) -> dict:
             "payload": "encode 10 L per stripe + decode 10 L per stripe with >= 1 erasure",
             "device_resident_data_GiB_s": round((data + dec_data) / t_dev / 2**30, 2),
             "device_resident": "one ragged encode + one ragged reconstruct launch over all stripes",
-            "end_to_end_data_GiB_s": round((data + dec_data) / t_e2e / 2**30, 2),
-            "raw": {"payload_bytes": data + dec_data, "e2e": [w0, w1], "device_s": t_dev}}
+            "encode": {"kernel": "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)", "ms_median": round(enc_ms, 4),
+                       "algorithmic_bytes": enc_hbm, "GB_s_hbm": round(enc_hbm / enc_ms / 1e6, 1),
+                       "frac": round(enc_hbm / enc_ms / 1e6 / HBM_PEAK_GBPS, 4)},
+            "decode": {"kernel": "rs104_ragged_kernel<DEC=true>", "ms_median": round(dec_ms, 4),
+                       "algorithmic_bytes": dec_hbm, "GB_s_hbm": round(dec_hbm / dec_ms / 1e6, 1),
+                       "frac": round(dec_hbm / dec_ms / 1e6 / HBM_PEAK_GBPS, 4)},
+            "end_to_end_stripes": len(sub_idx),
+            "end_to_end_data_GiB_s": round(e2e_payload / t_e2e / 2**30, 2),
+            "raw": {"payload_bytes": e2e_payload, "e2e": [w0, w1], "device_s": t_dev}}
+
+
+def packed_layout_pass(rs, S: int, L: int, masks, rank: int, reps: int) -> dict:
+    """The same encode + decode on a PACKED [S, 14, L] batch (shard stride =
+    L, what hec_gpu_*_batch callers that do not pad get), timed per launch with
+    HIP events beside the padded headline batch (after it, untimed by the
+    headline clock)."""
+    import torch
+    import helyim_amd.batch as B
+    tp = torch.empty((S, N_TOTAL, L), dtype=torch.uint8, device="cuda")
+    B.fill_stripes_splitmix(tp, K_DATA, rank_seed_base(rank))
+    B.encode_batch(rs, tp)  # warm-up
+    B.reconstruct_batch(rs, tp, masks)
+    st = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps + 1)]
+    ev[0].record(st)
+    for i in range(reps):
+        B.encode_batch(rs, tp)
+        ev[2 * i + 1].record(st)
+        B.reconstruct_batch(rs, tp, masks)
+        ev[2 * i + 2].record(st)
+    torch.cuda.synchronize()
+    enc = float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)]))
+    dec = float(np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(reps)]))
+    del tp
+    torch.cuda.empty_cache()
+    b = S * N_TOTAL * L
+    return {"shard_stride": L, "reps": reps, "encode_ms_median": round(enc, 4), "decode_ms_median": round(dec, 4),
+            "encode_frac": round(b / enc / 1e6 / HBM_PEAK_GBPS, 4), "decode_frac": round(b / dec / 1e6 / HBM_PEAK_GBPS, 4),
+            "data_GiB_s": round(2 * S * K_DATA * L / ((enc + dec) * 1e-3) / 2**30, 2)}
 
 
 def init_control_plane() -> None:
@@ -439,6 +487,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the end-to-end and mixed-workload sections")
+    ap.add_argument("--no-packed", action="store_true", help="skip the packed-layout pass beside the padded batch")
     ap.add_argument("--allow-shared-gpu", action="store_true",
                     help="rehearsal: allow more ranks than visible GPUs (ranks share devices round-robin)")
     ap.add_argument("--dry-run", action="store_true",
@@ -584,6 +633,10 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
         chk_ok &= bool(np.array_equal(t[0:2, K_DATA:].cpu().numpy(), ref))
     t_shard_stride = t.stride(1)
     del t
+    packed = None
+    if args.shard_pad and not args.no_packed:
+        torch.cuda.empty_cache()
+        packed = packed_layout_pass(rs, S, L, masks, rank, max(3, args.steps // 2))
     # every rank's verification counts: the job is verified only if all are
     chk_ok = reduce_max(0.0 if chk_ok else 1.0, world) == 0.0
     per_rank = gather({"rank": rank, "device": device, "seed_base": rank_seed_base(rank), "numa": numa,
@@ -609,6 +662,11 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
         # the aggregate shows the shared host-memory / PCIe limit
         barrier()
         e2e = e2e_section(rs, rank)
+        if world == 1 and torch.cuda.device_count() > 1:
+            # one process, every visible GPU: one host call split over them
+            # (hec_host_*_batch_multi), the in-process multi-GPU host path
+            nd = torch.cuda.device_count()
+            extras["end_to_end_multi_gpu"] = e2e_section(rs, rank, S=256 * nd, devices=list(range(nd)))
         barrier()
         mixed = mixed_section(rs, rank)
         e2e_all = gather(e2e, world)
@@ -675,6 +733,7 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
                        "data_GiB_s": round(S * K_DATA * L / (dec_ms * 1e-3) / 2**30, 1),
                        "frac": round(dec_gbps / HBM_PEAK_GBPS, 4),
                        "traffic": prof.get("decode_hbm_bytes_per_launch")},
+            "packed_layout": packed,
             "verified": chk_ok,
             "ranks": per_rank,
         }

@@ -55,6 +55,8 @@ SIGNATURES = {
     "hec_gpu_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P]),
     "hec_host_encode_batch": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32]),
     "hec_host_reconstruct_batch": (_I, [_P, _P, _U64, _U64, _U64, _U32, _P, _P]),
+    "hec_host_encode_batch_multi": (_I, [_P, _P, _S, _P, _U64, _U64, _P, _U64, _U64, _U64, _U32]),
+    "hec_host_reconstruct_batch_multi": (_I, [_P, _P, _S, _P, _U64, _U64, _U64, _U32, _P, _P]),
     "hec_gpu_encode_ragged": (_I, [_P, _P, _P, _U32, _P]),
     "hec_gpu_reconstruct_ragged": (_I, [_P, _P, _P, _U32, _P, _P]),
     "hec_gpu_fill_splitmix": (_I, [_P, _U64, _U64, _U32, _U64, _P]),
@@ -92,6 +94,7 @@ SIGNATURES = {
     "hec_set_decode_vector_bytes": (_I, [_I]),
     "hec_set_encode_vector_bytes": (_I, [_I]),
     "hec_set_encode_kernel": (_I, [_I]),
+    "hec_set_ragged_encode_remap": (_I, [_I]),
     "hec_set_host_zero_copy": (_I, [_I]),
     "hec_set_xcd_parts": (_I, [_I]),
     "hec_set_chunk_rotation": (_I, [_I]),

@@ -90,20 +90,37 @@ def _check_host(t: torch.Tensor, rs: ReedSolomon):
         raise ValueError(f"expected {rs.total_shard_count()} shards per stripe, got {t.shape[1]}")
 
 
-def host_encode_batch(rs: ReedSolomon, stripes: torch.Tensor) -> None:
+def _device_list(devices):
+    """devices -> (ctypes int array, count) for the *_multi calls."""
+    import ctypes
+    ds = [int(d) for d in devices]
+    if not ds:
+        raise ValueError("empty device list")
+    return (ctypes.c_int * len(ds))(*ds), len(ds)
+
+
+def host_encode_batch(rs: ReedSolomon, stripes: torch.Tensor, devices=None) -> None:
     """Host-memory stripes[S, total, L] (pin_memory() for full PCIe rate):
-    parity computed on the GPU, pipelined H2D -> kernel -> D2H."""
+    parity computed on the GPU, pipelined H2D -> kernel -> D2H. devices (a
+    list of GPU ids, repeats allowed): contiguous stripe ranges, one per entry,
+    coded concurrently (hec_host_encode_batch_multi); None = the current
+    device."""
     _check_host(stripes, rs)
     k = rs.data_shard_count()
     S, n, L = stripes.shape
     st, sh = stripes.stride(0), stripes.stride(1)
     base = stripes.data_ptr()
-    check(lib.hec_host_encode_batch(rs.handle, base, st, sh, base + k * sh, st, sh, L, S))
+    if devices is None:
+        check(lib.hec_host_encode_batch(rs.handle, base, st, sh, base + k * sh, st, sh, L, S))
+        return
+    arr, nd = _device_list(devices)
+    check(lib.hec_host_encode_batch_multi(rs.handle, arr, nd, base, st, sh, base + k * sh, st, sh, L, S))
 
 
-def host_reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks) -> int:
+def host_reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks, devices=None) -> int:
     """Host-memory in-place reconstruct; returns the number of skipped stripes
-    (fewer than data_shards present)."""
+    (fewer than data_shards present). devices: as host_encode_batch
+    (hec_host_reconstruct_batch_multi)."""
     import ctypes
     import numpy as np
     _check_host(stripes, rs)
@@ -112,8 +129,13 @@ def host_reconstruct_batch(rs: ReedSolomon, stripes: torch.Tensor, present_masks
     if m.size != S:
         raise ValueError(f"{m.size} present masks for {S} stripes")
     bad = ctypes.c_uint32(0)
-    check(lib.hec_host_reconstruct_batch(rs.handle, stripes.data_ptr(), stripes.stride(0), stripes.stride(1), L,
-                                         S, m.ctypes.data, ctypes.byref(bad)))
+    if devices is None:
+        check(lib.hec_host_reconstruct_batch(rs.handle, stripes.data_ptr(), stripes.stride(0), stripes.stride(1),
+                                             L, S, m.ctypes.data, ctypes.byref(bad)))
+    else:
+        arr, nd = _device_list(devices)
+        check(lib.hec_host_reconstruct_batch_multi(rs.handle, arr, nd, stripes.data_ptr(), stripes.stride(0),
+                                                   stripes.stride(1), L, S, m.ctypes.data, ctypes.byref(bad)))
     return int(bad.value)
 
 

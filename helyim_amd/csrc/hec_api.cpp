@@ -707,6 +707,11 @@ int hec_set_encode_kernel(int kind) {
     return HEC_OK;
 }
 
+int hec_set_ragged_encode_remap(int on) {
+    update_launch_config([&](LaunchConfig& c) { c.ragged_encode_remap = on ? 1 : 0; });
+    return HEC_OK;
+}
+
 int hec_set_host_staging(uint64_t max_bytes) {
     host_staging_max() = max_bytes;
     return HEC_OK;

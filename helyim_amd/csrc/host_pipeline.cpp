@@ -41,6 +41,7 @@ struct Pipeline {
         hslot_cap = bytes;
         return HEC_OK;
     }
+    int init() { return HEC_OK; }  // streams and slots are made on first use (reserve)
     ~Pipeline() {
         for (auto& h : hslot) (void)hipHostFree(h);
         for (auto& e : hdone)
@@ -81,18 +82,23 @@ struct Pipeline {
     }
 };
 
-std::mutex g_pipe_mu;
-std::map<int, std::unique_ptr<Pipeline>> g_pipes;
-
-int pipeline(Pipeline** out) {
+// Per-device pool of pipelines (SlotPool, hec_internal.hpp): concurrent host
+// batches on one device -- other threads, or two ranges of one multi-device
+// call on the same GPU -- each lease their own streams and slots.
+int lease_pipeline(Lease<Pipeline>& out) {
+    static std::mutex mu;
+    static auto* reg = new std::map<int, std::unique_ptr<SlotPool<Pipeline>>>();  // process lifetime
     int dev;
     int rc = current_device(&dev);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(g_pipe_mu);
-    auto& p = g_pipes[dev];
-    if (!p) p.reset(new Pipeline());
-    *out = p.get();
-    return HEC_OK;
+    SlotPool<Pipeline>* pool;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto& p = (*reg)[dev];
+        if (!p) p.reset(new SlotPool<Pipeline>());
+        pool = p.get();
+    }
+    return pool->lease(out);
 }
 
 // Copy `rows` rows of `width` bytes with pitches (2D; 1D when both are dense).
@@ -142,6 +148,54 @@ uint32_t chunk_stripes(uint64_t shard_len, int n, uint32_t n_stripes) {
     return uint32_t(std::min<uint64_t>(c, n_stripes));
 }
 
+// One host batch over a device set (contiguous stripe ranges
+// per GPU). Range r = stripes [S*r/R, S*(r+1)/R) of R = min(n_devices, S)
+// ranges runs on devices[r] from its own host thread: hipSetDevice, CPUs bound
+// to that GPU's NUMA node (hec_bind_thread_to_device), and the single-device
+// host path, which leases its own pipeline (streams, device slots, pinned
+// staging on that node). A device listed twice runs two ranges concurrently on
+// two pipelines. Every range runs to its end; the call returns the status of
+// the first failing range in list order (its detail prefixed with the range).
+int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
+                      const std::function<int(uint32_t s0, uint32_t count, size_t range)>& fn) {
+    if (!devices || n_devices == 0) return fail(HEC_ERR_INVALID_ARGUMENT, "empty device list");
+    int count = 0;
+    HEC_TRY(hec_device_count(&count));
+    for (size_t r = 0; r < n_devices; ++r)
+        if (devices[r] < 0 || devices[r] >= count)
+            return fail(HEC_ERR_INVALID_ARGUMENT,
+                        "device " + std::to_string(devices[r]) + " of " + std::to_string(count) + " in the list");
+    if (n_stripes == 0) return HEC_OK;
+    const size_t R = std::min<size_t>(n_devices, n_stripes);
+    std::vector<int> rcs(R, HEC_OK);
+    std::vector<std::string> details(R);
+    std::vector<std::thread> th;
+    th.reserve(R);
+    for (size_t r = 0; r < R; ++r) {
+        const uint32_t s0 = uint32_t(uint64_t(n_stripes) * r / R);
+        const uint32_t s1 = uint32_t(uint64_t(n_stripes) * (r + 1) / R);
+        th.emplace_back([&, r, s0, s1] {
+            const hipError_t e = hipSetDevice(devices[r]);
+            if (e != hipSuccess) {
+                rcs[r] = hip_fail(e, "hipSetDevice");
+            } else {
+                (void)hec_bind_thread_to_device(devices[r], nullptr);  // placement only: no-op when unknown
+                rcs[r] = fn(s0, s1 - s0, r);
+            }
+            if (rcs[r]) details[r] = hec_last_error_detail();
+        });
+    }
+    for (auto& t : th) t.join();
+    for (size_t r = 0; r < R; ++r)
+        if (rcs[r]) {
+            const uint32_t s0 = uint32_t(uint64_t(n_stripes) * r / R);
+            const uint32_t s1 = uint32_t(uint64_t(n_stripes) * (r + 1) / R);
+            return fail(rcs[r], "device " + std::to_string(devices[r]) + " stripes [" + std::to_string(s0) + ", " +
+                                    std::to_string(s1) + "): " + details[r]);
+        }
+    return HEC_OK;
+}
+
 }  // namespace
 }  // namespace hec
 
@@ -162,9 +216,9 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
         return rc;
     GeomDevice* gd;
     if ((rc = geom_device(rs, &gd))) return rc;
-    Pipeline* p;
-    if ((rc = pipeline(&p))) return rc;
-    std::lock_guard<std::mutex> lk(p->mu);
+    Lease<Pipeline> lease;
+    if ((rc = lease_pipeline(lease))) return rc;
+    Pipeline* p = lease.sc;
     const int k = rs->k, m = rs->m;
     uint8_t *zd, *zp;
     if (host_device_view(h_data, batch_span(data_stripe_stride, data_shard_stride, k, shard_len, n_stripes), &zd) &&
@@ -256,9 +310,9 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
     if ((rc = check_strided("shards", uint32_t(rs->n), stripe_stride, shard_stride, shard_len, n_stripes))) return rc;
     GeomDevice* gd;
     if ((rc = geom_device(rs, &gd))) return rc;
-    Pipeline* p;
-    if ((rc = pipeline(&p))) return rc;
-    std::lock_guard<std::mutex> lk(p->mu);
+    Lease<Pipeline> lease;
+    if ((rc = lease_pipeline(lease))) return rc;
+    Pipeline* p = lease.sc;
     const int k = rs->k, n = rs->n;
     const uint32_t full = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
     uint8_t* zs;
@@ -403,6 +457,43 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
     }
     for (int q = 0; q < kDepth; ++q) HEC_HIP(hipStreamSynchronize(p->streams[q]));
     if (n_bad_stripes) *n_bad_stripes = bad;
+    return HEC_OK;
+}
+
+int hec_host_encode_batch_multi(const hec_rs_t* rs, const int* devices, size_t n_devices, const uint8_t* h_data,
+                                uint64_t data_stripe_stride, uint64_t data_shard_stride, uint8_t* h_parity,
+                                uint64_t parity_stripe_stride, uint64_t parity_shard_stride, uint64_t shard_len,
+                                uint32_t n_stripes) {
+    if (!rs || !h_data || !h_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    int rc;
+    if ((rc = check_strided("data", uint32_t(rs->k), data_stripe_stride, data_shard_stride, shard_len, n_stripes)) ||
+        (rc = check_strided("parity", uint32_t(rs->m), parity_stripe_stride, parity_shard_stride, shard_len,
+                            n_stripes)))
+        return rc;
+    return run_device_ranges(devices, n_devices, n_stripes, [&](uint32_t s0, uint32_t c, size_t) {
+        return hec_host_encode_batch(rs, h_data + s0 * data_stripe_stride, data_stripe_stride, data_shard_stride,
+                                     h_parity + s0 * parity_stripe_stride, parity_stripe_stride, parity_shard_stride,
+                                     shard_len, c);
+    });
+}
+
+int hec_host_reconstruct_batch_multi(const hec_rs_t* rs, const int* devices, size_t n_devices, uint8_t* h_shards,
+                                     uint64_t stripe_stride, uint64_t shard_stride, uint64_t shard_len,
+                                     uint32_t n_stripes, const uint32_t* h_present_masks, uint32_t* n_bad_stripes) {
+    if (!rs || !h_shards || !h_present_masks) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (n_bad_stripes) *n_bad_stripes = 0;
+    int rc;
+    if ((rc = check_strided("shards", uint32_t(rs->n), stripe_stride, shard_stride, shard_len, n_stripes))) return rc;
+    std::vector<uint32_t> bad(std::max<size_t>(n_devices, 1), 0);
+    rc = run_device_ranges(devices, n_devices, n_stripes, [&](uint32_t s0, uint32_t c, size_t r) {
+        return hec_host_reconstruct_batch(rs, h_shards + s0 * stripe_stride, stripe_stride, shard_stride, shard_len, c,
+                                          h_present_masks + s0, &bad[r]);
+    });
+    if (rc) return rc;
+    if (n_bad_stripes)
+        for (uint32_t b : bad) *n_bad_stripes += b;
     return HEC_OK;
 }
 

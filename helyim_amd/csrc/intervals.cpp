@@ -353,10 +353,11 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     ra.tabs = decode ? gd->decode_dense.tabs : gd->encode.tabs;
     ra.lut = decode ? gd->decode_dense.lut : nullptr;
     ra.bad_count = d_bad;
-    // XCD eighths for the ragged decode (+2% on the bench batch, with the
-    // no-op skip +10% on the mixed workload's decode); the bit-sliced ragged
-    // encode measured 1% slower with it (profiles/r02/ab_ragged_remap_skip.jsonl)
-    ra.xcd_remap = decode && cfg.xcd_remap == 1 ? 1u : 0u;
+    // XCD eighths: the ragged decode +2% on the bench batch (with the no-op
+    // skip +10% on the mixed workload, profiles/r02/ab_ragged_remap_skip.jsonl);
+    // the bit-sliced ragged encode +2% at 512 mixed stripes, +7% at 4096 and
+    // +9% on uniform 4 MiB stripes (profiles/r03/sweep_mixed2.jsonl)
+    ra.xcd_remap = (decode ? cfg.xcd_remap == 1 : cfg.ragged_encode_remap != 0) ? 1u : 0u;
     if (n_blocks == 0) {  // every stripe already complete (upstream no-op)
         HEC_HIP(hipEventRecord(slot.free, stream));
         return HEC_OK;

@@ -928,14 +928,36 @@ static hipError_t launch_rs104_pair(ApplyArgs a, const LaunchConfig& cfg, hipStr
     return hipGetLastError();
 }
 
-template <bool DEC, bool XORONLY>
-static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
-    const int vb = DEC ? cfg.dec_vec_bytes : cfg.enc_vec_bytes;
+// The kernel an aligned RS(10,4) batch with the fast plan layout runs, shared
+// by launch_apply and the name functions so a reported name is the kernel
+// that runs (speed-only knobs; every choice gives identical bytes).
+enum class Rs104Kind { Apply, Bitslice, Narrow, Pair, Wide };
+struct Rs104Pick {
+    Rs104Kind kind;
+    int vb;  // Narrow: bytes per lane per shard (8 or 4)
+};
+static bool rs104_fast_ok(uint64_t len, const LaunchConfig& cfg);
+static bool rs104_bitslice_ok(uint64_t len, const LaunchConfig& cfg);
+static Rs104Pick rs104_pick(uint64_t len, uint64_t n_stripes, bool dec, const LaunchConfig& cfg) {
+    const uint64_t items = (len + 4095) / 4096 * n_stripes;
+    if (!rs104_fast_ok(len, cfg) || items > kMaxLaunchBlocks) return {Rs104Kind::Apply, 16};
+    if (!dec && rs104_bitslice_ok(len, cfg)) return {Rs104Kind::Bitslice, 16};
+    const int vb = dec ? cfg.dec_vec_bytes : cfg.enc_vec_bytes;
     const uint64_t narrow = uint64_t(kThreads) * uint64_t(vb);  // column range per workgroup
     // (launch_apply sizes its stripe ranges for 4 KiB chunks; a narrow launch
     // that would pass kMaxLaunchBlocks workgroups takes the 16-byte kernel)
-    if (vb < 16 && cfg.vec_per_thread == 1 && a.len % narrow == 0 && fast_map_ok(cfg, a.len) &&
-        cfg.wg_threads == kThreads && (a.len / narrow) * a.n_stripes <= kMaxLaunchBlocks) {
+    if (vb < 16 && cfg.vec_per_thread == 1 && len % narrow == 0 && fast_map_ok(cfg, len) &&
+        cfg.wg_threads == kThreads && (len / narrow) * n_stripes <= kMaxLaunchBlocks)
+        return {Rs104Kind::Narrow, vb};
+    if (cfg.vec_per_thread == 2 && len % (2 * uint64_t(kThreads) * kVecBytes) == 0) return {Rs104Kind::Pair, 16};
+    return {Rs104Kind::Wide, 16};
+}
+
+template <bool DEC, bool XORONLY>
+static hipError_t launch_rs104(const ApplyArgs& a, const Rs104Pick& pick, const LaunchConfig& cfg,
+                               hipStream_t stream) {
+    if (pick.kind == Rs104Kind::Narrow) {
+        const uint64_t narrow = uint64_t(kThreads) * uint64_t(pick.vb);
         ApplyArgs b = a;
         b.chunks_per_stripe = uint32_t(a.len / narrow);
         b.n_items = uint64_t(b.chunks_per_stripe) * a.n_stripes;
@@ -944,7 +966,7 @@ static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipS
         b.chunk_rot = uint32_t(cfg.chunk_rot);
         set_fast_map(b, b.n_items, b.chunks_per_stripe);
         const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-        if (vb == 8)
+        if (pick.vb == 8)
             hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x2>), dim3(uint32_t(b.n_items)), dim3(kThreads),
                                lds, stream, b);
         else
@@ -952,8 +974,7 @@ static hipError_t launch_rs104(const ApplyArgs& a, const LaunchConfig& cfg, hipS
                                lds, stream, b);
         return hipGetLastError();
     }
-    if (cfg.vec_per_thread == 2 && a.len % (2 * uint64_t(kThreads) * kVecBytes) == 0)
-        return launch_rs104_pair<DEC, XORONLY>(a, cfg, stream);
+    if (pick.kind == Rs104Kind::Pair) return launch_rs104_pair<DEC, XORONLY>(a, cfg, stream);
     switch (cfg.wg_threads) {
         case 512: return launch_rs104_tb<DEC, XORONLY, 512>(a, cfg, stream);
         case 1024: return launch_rs104_tb<DEC, XORONLY, 1024>(a, cfg, stream);
@@ -991,28 +1012,41 @@ static bool rs104_bitslice_ok(uint64_t len, const LaunchConfig& cfg) {
     return cfg.bitslice && cfg.mode == 0 && len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0;
 }
 
+// Name of the kernel rs104_pick selects (one stripe: the name functions take
+// a shard length only) and its XOR-only diagnostic twin (mode 1).
+static const char* rs104_name(const Rs104Pick& p, bool dec, bool xo) {
+    switch (p.kind) {
+        case Rs104Kind::Apply:
+            return xo ? "rs_apply_kernel<10, XORONLY=true> (diagnostic)" : "rs_apply_kernel<10> (table lookup)";
+        case Rs104Kind::Bitslice: return "rs104_bs_encode_kernel (bit-sliced)";
+        case Rs104Kind::Narrow:
+            if (p.vb == 8)
+                return dec ? (xo ? "rs104_narrow_kernel<DEC=true, XORONLY=true, 8 B per lane> (diagnostic)"
+                                 : "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)")
+                           : (xo ? "rs104_narrow_kernel<DEC=false, XORONLY=true, 8 B per lane> (diagnostic)"
+                                 : "rs104_narrow_kernel<DEC=false, 8 B per lane> (table lookup)");
+            return dec ? (xo ? "rs104_narrow_kernel<DEC=true, XORONLY=true, 4 B per lane> (diagnostic)"
+                             : "rs104_narrow_kernel<DEC=true, 4 B per lane> (table lookup)")
+                       : (xo ? "rs104_narrow_kernel<DEC=false, XORONLY=true, 4 B per lane> (diagnostic)"
+                             : "rs104_narrow_kernel<DEC=false, 4 B per lane> (table lookup)");
+        case Rs104Kind::Pair:
+            return dec ? (xo ? "rs104_pair_kernel<DEC=true, XORONLY=true> (diagnostic)"
+                             : "rs104_pair_kernel<DEC=true> (table lookup)")
+                       : (xo ? "rs104_pair_kernel<DEC=false, XORONLY=true> (diagnostic)"
+                             : "rs104_pair_kernel<DEC=false> (table lookup)");
+        default:
+            return dec ? (xo ? "rs104_kernel<DEC=true, XORONLY=true> (diagnostic)" : "rs104_kernel<DEC=true> (table lookup)")
+                       : (xo ? "rs104_kernel<DEC=false, XORONLY=true> (diagnostic)"
+                             : "rs104_kernel<DEC=false> (table lookup)");
+    }
+}
+
 const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
-    if (!rs104_fast_ok(len, cfg)) return "rs_apply_kernel<10> (table lookup)";
-    if (cfg.mode == 1) return "rs104_kernel<DEC=true, XORONLY=true> (diagnostic)";
-    if (cfg.vec_per_thread == 2) return "rs104_pair_kernel<DEC=true> (table lookup)";
-    if (cfg.dec_vec_bytes < 16 && len % (uint64_t(kThreads) * cfg.dec_vec_bytes) == 0 && fast_map_ok(cfg, len) &&
-        cfg.wg_threads == kThreads)
-        return cfg.dec_vec_bytes == 8 ? "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)"
-                                      : "rs104_narrow_kernel<DEC=true, 4 B per lane> (table lookup)";
-    return "rs104_kernel<DEC=true> (table lookup)";
+    return rs104_name(rs104_pick(len, 1, true, cfg), true, cfg.mode == 1);
 }
 
 const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
-    if (!rs104_fast_ok(len, cfg))
-        return cfg.mode == 1 ? "rs_apply_kernel<10, XORONLY=true> (diagnostic)" : "rs_apply_kernel<10> (table lookup)";
-    if (cfg.mode == 1) return "rs104_kernel<DEC=false, XORONLY=true> (diagnostic)";
-    if (rs104_bitslice_ok(len, cfg)) return "rs104_bs_encode_kernel (bit-sliced)";
-    if (cfg.enc_vec_bytes < 16 && len % (uint64_t(kThreads) * cfg.enc_vec_bytes) == 0 && fast_map_ok(cfg, len) &&
-        cfg.wg_threads == kThreads)
-        return cfg.enc_vec_bytes == 8 ? "rs104_narrow_kernel<DEC=false, 8 B per lane> (table lookup)"
-                                      : "rs104_narrow_kernel<DEC=false, 4 B per lane> (table lookup)";
-    if (cfg.vec_per_thread == 2) return "rs104_pair_kernel<DEC=false> (table lookup)";
-    return "rs104_kernel<DEC=false> (table lookup)";
+    return rs104_name(rs104_pick(len, 1, false, cfg), false, cfg.mode == 1);
 }
 
 hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
@@ -1037,11 +1071,13 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
         }
         return hipSuccess;
     }
-    if (a.fast104 && aligned && rs104_fast_ok(a.len, cfg) && items <= kMaxLaunchBlocks) {
-        if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, cfg, stream)
-                                          : launch_rs104<true, false>(a, cfg, stream);
-        if (rs104_bitslice_ok(a.len, cfg)) return launch_rs104_bs_cfg(a, cfg, stream);
-        return cfg.mode == 1 ? launch_rs104<false, true>(a, cfg, stream) : launch_rs104<false, false>(a, cfg, stream);
+    const Rs104Pick pick = rs104_pick(a.len, a.n_stripes, a.masks != nullptr, cfg);
+    if (a.fast104 && aligned && pick.kind != Rs104Kind::Apply) {
+        if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, pick, cfg, stream)
+                                          : launch_rs104<true, false>(a, pick, cfg, stream);
+        if (pick.kind == Rs104Kind::Bitslice) return launch_rs104_bs_cfg(a, cfg, stream);
+        return cfg.mode == 1 ? launch_rs104<false, true>(a, pick, cfg, stream)
+                             : launch_rs104<false, false>(a, pick, cfg, stream);
     }
     if (nin == 10 && aligned && cfg.mode == 1) {
         switch (cfg.vec_per_thread) {

@@ -116,6 +116,7 @@ struct LaunchConfig {
     int dec_vec_bytes = 8;       // RS(10,4) decode bytes per lane per shard: 8 (default: dwordx2, 2 KiB
                                  // per workgroup, on shard lengths a multiple of 2 KiB), 16 or 4 (speed only)
     int enc_vec_bytes = 16;      // RS(10,4) table encode bytes per lane per shard: 16 (default), 8 or 4 (speed only)
+    int ragged_encode_remap = 1; // 1: XCD eighths for ragged encodes (default; 0 = dispatch order; speed only)
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
                                  // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
                                  // multiply (speed only)
@@ -126,8 +127,9 @@ struct LaunchConfig {
 hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
                         hipStream_t stream);
 
-// Name of the kernel an aligned RS(10,4) device encode of this shard length
-// runs under cfg (introspection for benchmarks and profiles).
+// Name of the kernel an aligned RS(10,4) device encode of one stripe of this
+// shard length runs under cfg (introspection for benchmarks and profiles; the
+// same choice launch_apply makes, rs_kernels.hip rs104_pick).
 const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg);
 // Same for an aligned in-place RS(10,4) device batch reconstruct.
 const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg);

@@ -52,8 +52,10 @@ def bind_host_to_device(device: int) -> dict:
 class HostBuffer:
     """Pinned host memory on the current device's NUMA node (hec_host_alloc),
     GPU-addressable, exposed as a numpy array (``.array``) or a torch CPU
-    tensor view (``.tensor(shape)``). Freed by ``close()`` or on collection;
-    views must not outlive it."""
+    tensor view (``.tensor(shape)``). Every view holds a reference to this
+    object (through the ctypes array under it), so collection -- and the
+    ``hec_host_free`` in ``__del__`` -- waits for the last view; an explicit
+    ``close()`` frees at once and must come after the views are gone."""
 
     def __init__(self, nbytes: int):
         import numpy as np
@@ -61,7 +63,9 @@ class HostBuffer:
         check(lib.hec_host_alloc(nbytes, ctypes.byref(p)))
         self._ptr = p.value
         self.nbytes = nbytes
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self._ptr))
+        raw = (ctypes.c_uint8 * nbytes).from_address(self._ptr)
+        raw._owner = self  # numpy / torch views keep raw, raw keeps the owner alive
+        self.array = np.ctypeslib.as_array(raw)
 
     @property
     def ptr(self) -> int:

@@ -209,6 +209,28 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
                                uint64_t shard_stride, uint64_t shard_len, uint32_t n_stripes,
                                const uint32_t* h_present_masks, uint32_t* n_bad_stripes);
 
+/* One host batch spread over several GPUs of this process (SURVEY.md §8e:
+ * contiguous stripe ranges per GPU; helyim's volume server is one process,
+ * helyim-store/src/server.rs:451-506, so without this one call is capped by
+ * one GPU's PCIe link). devices[0..n_devices) may repeat a device (two
+ * concurrent ranges on it). Range r = stripes [S*r/R, S*(r+1)/R), R =
+ * min(n_devices, n_stripes), runs on devices[r] from its own host thread
+ * (CPUs bound to that GPU's NUMA node) through hec_host_encode_batch /
+ * hec_host_reconstruct_batch, with its own streams and staging. Synchronous:
+ * returns when every range is done; on failure the status of the first
+ * failing range in list order (hec_last_error_detail names the range).
+ * Arguments and results otherwise as the single-device calls;
+ * *n_bad_stripes is the sum over ranges. An empty list or a device out of
+ * range -> HEC_ERR_INVALID_ARGUMENT before any work. */
+int hec_host_encode_batch_multi(const hec_rs_t* rs, const int* devices, size_t n_devices,
+                                const uint8_t* h_data, uint64_t data_stripe_stride, uint64_t data_shard_stride,
+                                uint8_t* h_parity, uint64_t parity_stripe_stride, uint64_t parity_shard_stride,
+                                uint64_t shard_len, uint32_t n_stripes);
+int hec_host_reconstruct_batch_multi(const hec_rs_t* rs, const int* devices, size_t n_devices,
+                                     uint8_t* h_shards, uint64_t stripe_stride, uint64_t shard_stride,
+                                     uint64_t shard_len, uint32_t n_stripes, const uint32_t* h_present_masks,
+                                     uint32_t* n_bad_stripes);
+
 /* Ragged device batches (RS(10,4)): every stripe has its own length, shard
  * stride and erasure pattern -- BASELINE config 5's mixed 64 KiB-4 MiB
  * stripes in ONE launch. Stripe j's shard i is at d_base + offset + i *
@@ -391,6 +413,11 @@ int hec_set_encode_vector_bytes(int bytes);
  * XOR program; the default), 0 = table-lookup GF multiply. Both give identical
  * parity (parity-tested); speed only. Returns HEC_OK. */
 int hec_set_encode_kernel(int kind);
+/* Ragged device encodes (hec_gpu_encode_ragged): 1 = the workgroups of one
+ * XCD take a contiguous eighth of the launch's column ranges, as the decodes
+ * do with xcd_remap 1 (default; 3-9% faster on the mixed workload, DESIGN.md
+ * §4), 0 = dispatch order. Speed only. Returns HEC_OK. */
+int hec_set_ragged_encode_remap(int on);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables

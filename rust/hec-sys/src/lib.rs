@@ -121,6 +121,14 @@ extern "C" {
     pub fn hec_host_reconstruct_batch(rs: *const hec_rs_t, h_shards: *mut u8, stripe_stride: u64,
                                       shard_stride: u64, shard_len: u64, n_stripes: u32,
                                       h_present_masks: *const u32, n_bad_stripes: *mut u32) -> c_int;
+    pub fn hec_host_encode_batch_multi(rs: *const hec_rs_t, devices: *const c_int, n_devices: usize,
+                                       h_data: *const u8, data_stripe_stride: u64, data_shard_stride: u64,
+                                       h_parity: *mut u8, parity_stripe_stride: u64, parity_shard_stride: u64,
+                                       shard_len: u64, n_stripes: u32) -> c_int;
+    pub fn hec_host_reconstruct_batch_multi(rs: *const hec_rs_t, devices: *const c_int, n_devices: usize,
+                                            h_shards: *mut u8, stripe_stride: u64, shard_stride: u64,
+                                            shard_len: u64, n_stripes: u32, h_present_masks: *const u32,
+                                            n_bad_stripes: *mut u32) -> c_int;
     pub fn hec_gpu_encode_ragged(rs: *const hec_rs_t, d_base: *mut u8, descs: *const hec_stripe_desc,
                                  n_stripes: u32, stream: *mut c_void) -> c_int;
     pub fn hec_gpu_reconstruct_ragged(rs: *const hec_rs_t, d_base: *mut u8, descs: *const hec_stripe_desc,
@@ -184,6 +192,7 @@ extern "C" {
     pub fn hec_set_decode_vector_bytes(bytes: c_int) -> c_int;
     pub fn hec_set_encode_vector_bytes(bytes: c_int) -> c_int;
     pub fn hec_set_encode_kernel(kind: c_int) -> c_int;
+    pub fn hec_set_ragged_encode_remap(on: c_int) -> c_int;
     pub fn hec_set_host_staging(max_bytes: u64) -> c_int;
     pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;
     pub fn hec_set_host_zero_copy(on: c_int) -> c_int;

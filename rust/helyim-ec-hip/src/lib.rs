@@ -81,10 +81,18 @@ impl ReedSolomon {
         unsafe { sys::hec_rs_total_shard_count(self.0) }
     }
 
-    /// Parity of shards[0..data] into shards[data..total], in place.
-    pub fn encode<T: AsMut<[u8]>>(&self, shards: &mut [T]) -> Result<(), Error> {
-        let lens: Vec<usize> = shards.iter_mut().map(|s| s.as_mut().len()).collect();
-        let ptrs: Vec<*mut u8> = shards.iter_mut().map(|s| s.as_mut().as_mut_ptr()).collect();
+    /// Parity of shards[0..data] into shards[data..total], in place. Upstream's
+    /// signature (reed_solomon_erasure 6.0.0 `ReedSolomon::encode<T, U>(&self,
+    /// shards: T)`), so `reed_solomon.encode(bufs.as_mut())` at
+    /// helyim-ec/src/encoder.rs:191 binds unchanged.
+    pub fn encode<T, U>(&self, mut shards: T) -> Result<(), Error>
+    where
+        T: AsRef<[U]> + AsMut<[U]>,
+        U: AsRef<[u8]> + AsMut<[u8]>,
+    {
+        let slices = shards.as_mut();
+        let lens: Vec<usize> = slices.iter().map(|s| s.as_ref().len()).collect();
+        let ptrs: Vec<*mut u8> = slices.iter_mut().map(|s| s.as_mut().as_mut_ptr()).collect();
         check(unsafe { sys::hec_rs_encode(self.0, ptrs.as_ptr(), lens.as_ptr(), ptrs.len()) })
     }
 
@@ -96,26 +104,44 @@ impl ReedSolomon {
         Ok(ok == 1)
     }
 
-    /// Upstream semantics: missing `None` slots are allocated `vec![0; len]`
-    /// and filled; on error the slots are left as they were.
-    pub fn reconstruct(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+    /// Upstream semantics and signature (`reconstruct<T: ReconstructShard<F>>(&self,
+    /// shards: &mut [T])`): `reconstruct(&mut bufs)` at encoder.rs:288 and
+    /// erasure_coding/mod.rs:426 binds unchanged. Missing `None` slots are
+    /// allocated `vec![0; len]` and filled; on error the slots are left as
+    /// they were.
+    pub fn reconstruct<T: ReconstructShard>(&self, shards: &mut [T]) -> Result<(), Error> {
         self.reconstruct_impl(shards, false)
     }
 
-    /// As `reconstruct`, but missing parity slots stay `None`.
-    pub fn reconstruct_data(&self, shards: &mut [Option<Vec<u8>>]) -> Result<(), Error> {
+    /// As `reconstruct`, but missing parity slots stay absent.
+    pub fn reconstruct_data<T: ReconstructShard>(&self, shards: &mut [T]) -> Result<(), Error> {
         self.reconstruct_impl(shards, true)
     }
 
-    fn reconstruct_impl(&self, shards: &mut [Option<Vec<u8>>], data_only: bool) -> Result<(), Error> {
-        let present: Vec<u8> = shards.iter().map(|s| s.is_some() as u8).collect();
-        let lens: Vec<usize> = shards.iter().map(|s| s.as_ref().map_or(0, |v| v.len())).collect();
+    fn reconstruct_impl<T: ReconstructShard>(&self, shards: &mut [T], data_only: bool) -> Result<(), Error> {
+        let present: Vec<u8> = shards.iter().map(|s| s.len().is_some() as u8).collect();
+        let lens: Vec<usize> = shards.iter().map(|s| s.len().unwrap_or(0)).collect();
         let len = lens.iter().copied().find(|&l| l > 0).unwrap_or(0);
         let k = self.data_shard_count();
-        for s in shards.iter_mut().filter(|s| s.is_none()) {
-            *s = Some(vec![0u8; len]);
+        let mut ptrs: Vec<*mut u8> = Vec::with_capacity(shards.len());
+        let mut init_err = None;
+        for s in shards.iter_mut() {
+            match s.get_or_initialize(len) {
+                Ok(b) => ptrs.push(b.as_mut_ptr()),
+                Err(e) => {
+                    init_err = Some(e);
+                    break;
+                }
+            }
         }
-        let ptrs: Vec<*mut u8> = shards.iter_mut().map(|s| s.as_mut().unwrap().as_mut_ptr()).collect();
+        if let Some(e) = init_err {
+            for (t, &p) in shards.iter_mut().zip(&present) {
+                if p == 0 {
+                    t.reset(); // nothing written: absent slots stay absent
+                }
+            }
+            return Err(e);
+        }
         let rc = unsafe {
             if data_only {
                 sys::hec_rs_reconstruct_data(self.0, ptrs.as_ptr(), lens.as_ptr(), present.as_ptr(), ptrs.len())
@@ -125,7 +151,7 @@ impl ReedSolomon {
         };
         for (i, (s, &p)) in shards.iter_mut().zip(&present).enumerate() {
             if p == 0 && (rc != 0 || (data_only && i >= k)) {
-                *s = None; // untouched on error; reconstruct_data leaves parity absent
+                s.reset(); // untouched on error; reconstruct_data leaves parity absent
             }
         }
         check(rc)
@@ -137,6 +163,18 @@ impl ReedSolomon {
     /// nothing is written and the error names the first failing stripe.
     pub fn reconstruct_batch(&self, stripes: &mut [Vec<Option<Vec<u8>>>]) -> Result<(), (Error, usize)> {
         let n = self.total_shard_count();
+        // hec_rs_reconstruct_batch reads exactly n entries per stripe: a stripe
+        // of another length would shift every later stripe's shards (and read
+        // past the arrays), so it is refused first, as upstream's per-call
+        // check_piece_count! does
+        for (j, st) in stripes.iter().enumerate() {
+            if st.len() < n {
+                return Err((Error::TooFewShards, j));
+            }
+            if st.len() > n {
+                return Err((Error::TooManyShards, j));
+            }
+        }
         let mut ptrs = Vec::with_capacity(stripes.len() * n);
         let mut lens = Vec::with_capacity(stripes.len() * n);
         let mut present = Vec::with_capacity(stripes.len() * n);
@@ -165,6 +203,48 @@ impl ReedSolomon {
             return Err((to_err(rc), bad));
         }
         Ok(())
+    }
+}
+
+/// The shard slots `reconstruct` accepts (upstream `ReconstructShard<F>` for
+/// `galois_8::Field`): `Option<Vec<u8>>` (absent = `None`, allocated on
+/// reconstruct) and `(buffer, present)` pairs whose buffer is caller storage.
+pub trait ReconstructShard {
+    /// Length of a present shard; `None` when the slot is absent.
+    fn len(&self) -> Option<usize>;
+    /// The slot's bytes, allocating `len` zero bytes for an absent
+    /// `Option` slot; an absent pair slot whose buffer is not `len` long is
+    /// `IncorrectShardSize`.
+    fn get_or_initialize(&mut self, len: usize) -> Result<&mut [u8], Error>;
+    /// Back to absent after a failed or data-only reconstruct.
+    fn reset(&mut self);
+}
+
+impl ReconstructShard for Option<Vec<u8>> {
+    fn len(&self) -> Option<usize> {
+        self.as_ref().map(|v| v.len())
+    }
+    fn get_or_initialize(&mut self, len: usize) -> Result<&mut [u8], Error> {
+        Ok(self.get_or_insert_with(|| vec![0u8; len]).as_mut_slice())
+    }
+    fn reset(&mut self) {
+        *self = None;
+    }
+}
+
+impl<T: AsRef<[u8]> + AsMut<[u8]>> ReconstructShard for (T, bool) {
+    fn len(&self) -> Option<usize> {
+        if self.1 { Some(self.0.as_ref().len()) } else { None }
+    }
+    fn get_or_initialize(&mut self, len: usize) -> Result<&mut [u8], Error> {
+        if !self.1 && self.0.as_ref().len() != len {
+            return Err(Error::IncorrectShardSize);
+        }
+        self.1 = true; // filled by the reconstruct (reset() undoes it on failure)
+        Ok(self.0.as_mut())
+    }
+    fn reset(&mut self) {
+        self.1 = false;
     }
 }
 

@@ -192,3 +192,52 @@ def test_strided_batch_geometry_checked_before_device():
     assert lib.hec_gpu_reconstruct_batch(rs.handle, P, 14 * L, L - 1, L, 2, P, None, None) == 66
     assert lib.hec_host_reconstruct_batch(rs.handle, P, 14 * L, L - 1, L, 2, masks, None) == 66
     assert lib.hec_host_reconstruct_batch(rs.handle, P, 1 << 63, L, L, 3, masks, None) == 66
+    # the one-call *_multi host batches check the geometry and the device list
+    # before starting any thread or device work
+    devs = (ctypes.c_int * 2)(0, 0)
+    for args in bad_encode:
+        assert lib.hec_host_encode_batch_multi(rs.handle, devs, 2, *args) == 66, args
+    assert lib.hec_host_reconstruct_batch_multi(rs.handle, devs, 2, P, 14 * L, L - 1, L, 2, masks, None) == 66
+    assert lib.hec_host_encode_batch_multi(rs.handle, None, 0, P, 14 * L, L, P, 14 * L, L, L, 2) != 0
+
+
+def test_kernel_name_follows_dispatch_under_every_knob():
+    """hec_{encode,decode}_kernel_name come from the same choice the launcher
+    makes (rs104_pick): the XOR-only mode names the diagnostic twin of the
+    kernel that runs (narrow at 4/8 B per lane, pair at 2 vectors per lane),
+    and 2 vectors per lane never reports the narrow kernel (it needs 1)."""
+    import helyim_amd as H
+    lib = H.lib
+    L = 1 << 20
+    try:
+        for mode in (0, 1):
+            for vpt in (1, 2):
+                for vb in (4, 8, 16):
+                    assert lib.hec_set_kernel_mode(mode) == 0
+                    assert lib.hec_set_launch_config(vpt, 0, 1, 0) == 0
+                    assert lib.hec_set_decode_vector_bytes(vb) == 0
+                    assert lib.hec_set_encode_vector_bytes(vb) == 0
+                    enc = lib.hec_encode_kernel_name(L).decode()
+                    dec = lib.hec_decode_kernel_name(L).decode()
+                    if vpt == 2:
+                        want_dec = "rs104_pair_kernel<DEC=true"
+                    elif vb < 16:
+                        want_dec = "rs104_narrow_kernel<DEC=true"
+                    else:
+                        want_dec = "rs104_kernel<DEC=true"
+                    assert dec.startswith(want_dec), (mode, vpt, vb, dec)
+                    assert (f"{vb} B per lane" in dec) == (vpt == 1 and vb < 16), dec
+                    if mode == 0:
+                        assert enc.startswith("rs104_bs_encode_kernel"), enc  # GF mode, 1 MiB: bit-sliced
+                    else:  # no bit-sliced XOR twin: the table kernels' twins
+                        want_enc = ("rs104_pair_kernel<DEC=false" if vpt == 2 else
+                                    "rs104_narrow_kernel<DEC=false" if vb < 16 else "rs104_kernel<DEC=false")
+                        assert enc.startswith(want_enc), (mode, vpt, vb, enc)
+                    for name in (enc, dec):
+                        assert ("XORONLY=true" in name) == (mode == 1) or name.startswith("rs104_bs"), name
+                        assert ("diagnostic" in name) == (mode == 1), name
+    finally:
+        lib.hec_set_kernel_mode(0)
+        lib.hec_set_launch_config(1, 0, 1, 0)
+        lib.hec_set_decode_vector_bytes(8)
+        lib.hec_set_encode_vector_bytes(16)

@@ -41,5 +41,8 @@ def test_bench_line_contract():
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3)
     assert r["algorithmic_bytes_per_launch"] == S * 14 * L  # 10 reads + 4 writes per stripe either way
     assert r["traffic"] is None  # the committed PMC bytes are of the 4096 x 1 MiB batch, not this one
+    pk = d["packed_layout"]  # the packed-stride rate beside the padded headline
+    assert pk["shard_stride"] == L and d["config"]["shard_stride"] == L + (64 << 10)
+    assert 0 < pk["encode_frac"] < 1 and 0 < pk["decode_frac"] < 1
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0 and cb["sample"]

@@ -124,3 +124,62 @@ def test_host_batches_generic_geometry(gpu, k, m, pin):
             a[s, int(i)] = 0xC3
     assert B.host_reconstruct_batch(rs, t, masks) == 0
     assert np.array_equal(a, want)
+
+
+# ---- one host batch over a device set (hec_host_*_batch_multi) -------------
+# The 1-GPU box repeats device 0: every range runs concurrently on its own
+# host thread, pipeline and streams, which is the code an 8-GPU node runs with
+# distinct ids. Range boundaries fall inside ragged stripe counts (S not a
+# multiple of the list length) and at one stripe per range.
+@pytest.mark.parametrize("devices,S,L,pin", [([0, 0], 7, 4096 + 3, True), ([0, 0, 0], 40, 1 << 20, True),
+                                             ([0, 0], 9, 65536 + 5, False), ([0] * 5, 3, 1000, True),
+                                             ([0, 0, 0, 0], 5, 17, False)])
+def test_host_batch_multi_device_encode_and_every_erasure_count(gpu, devices, S, L, pin):
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    t = _host_stripes(S, L, pin)
+    B.host_encode_batch(rs, t, devices=devices)
+    a = t.numpy()
+    want = a.copy()
+    want[:, 10:] = corc.encode_stripes(np.ascontiguousarray(a[:, :10]))
+    assert np.array_equal(a, want)
+    rng = np.random.default_rng(S * 131 + len(devices))
+    masks = np.full(S, (1 << 14) - 1, np.uint32)
+    for s in range(S):
+        e = s % 6  # 0..4 rebuilt, 5 counted as bad
+        for i in rng.choice(14, e, replace=False):
+            masks[s] &= ~np.uint32(1 << int(i))
+            a[s, int(i)] = 0xA5
+    bad = B.host_reconstruct_batch(rs, t, masks, devices=devices)
+    assert bad == sum(1 for s in range(S) if s % 6 == 5)
+    for s in range(S):
+        if s % 6 <= 4:
+            assert np.array_equal(a[s], want[s]), s
+
+
+def test_host_batch_multi_device_errors(gpu):
+    import ctypes
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    from helyim_amd.errors import DeviceError
+    rs = H.ReedSolomon(10, 4)
+    t = _host_stripes(4, 4096)
+    before = t.clone()
+    ndev = torch.cuda.device_count()
+    with pytest.raises(DeviceError) as ei:  # a device out of range fails before any work
+        B.host_encode_batch(rs, t, devices=[0, ndev])
+    assert "device" in str(ei.value)
+    assert torch.equal(t, before)
+    with pytest.raises(ValueError):
+        B.host_encode_batch(rs, t, devices=[])
+    devs = (ctypes.c_int * 2)(0, 0)  # no stripes: nothing to do
+    base = t.data_ptr()
+    assert H.lib.hec_host_encode_batch_multi(rs.handle, devs, 2, base, 14 * 4096, 4096, base + 40960, 14 * 4096,
+                                             4096, 4096, 0) == 0
+    # the multi-device call and the single-device call agree byte for byte
+    u = before.clone().pin_memory()
+    B.host_encode_batch(rs, t, devices=[0, 0, 0])
+    B.host_encode_batch(rs, u)
+    assert torch.equal(t, u)

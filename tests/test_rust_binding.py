@@ -44,3 +44,49 @@ def test_status_constants_match_header():
     assert consts
     for k, v in consts.items():
         assert codes[k] == v, k
+
+
+def _wrapper_src():
+    return open(os.path.join(ROOT, "rust", "helyim-ec-hip", "src", "lib.rs")).read()
+
+
+def _squash(s):
+    return re.sub(r"\s+", " ", s)
+
+
+def test_wrapper_signatures_match_upstream_shapes():
+    """helyim_ec_hip::ReedSolomon has upstream reed_solomon_erasure 6.0.0's
+    shapes for the three calls helyim makes, so the call sites bind unchanged
+    (INTEGRATION.md):
+      helyim-ec/src/encoder.rs:208-209, 249-250  ReedSolomon::new(DATA, PARITY)?
+      helyim-ec/src/encoder.rs:191               reed_solomon.encode(bufs.as_mut())?   (bufs: Vec<Vec<u8>>)
+      helyim-ec/src/encoder.rs:288               reed_solomon.reconstruct(&mut bufs)?  (Vec<Option<Vec<u8>>>)
+      helyim-store/src/erasure_coding/mod.rs:426 reed_solomon.reconstruct(&mut bufs)
+    upstream: encode<T, U>(&self, shards: T) where T: AsRef<[U]> + AsMut<[U]>,
+    U: AsRef<[u8]> + AsMut<[u8]>; reconstruct<T: ReconstructShard<F>>(&self,
+    shards: &mut [T]); new(data_shards: usize, parity_shards: usize)."""
+    src = _squash(_wrapper_src())
+    assert "pub fn new(data_shards: usize, parity_shards: usize) -> Result<Self, Error>" in src
+    m = re.search(r"pub fn encode<T, U>\(&self, mut shards: T\) -> Result<\(\), Error> where (.*?)\{", src)
+    assert m, "encode must take the shard container by value, generic over T and U"
+    bounds = m.group(1)
+    assert "T: AsRef<[U]> + AsMut<[U]>" in bounds and "U: AsRef<[u8]> + AsMut<[u8]>" in bounds, bounds
+    assert "pub fn reconstruct<T: ReconstructShard>(&self, shards: &mut [T]) -> Result<(), Error>" in src
+    assert "pub fn reconstruct_data<T: ReconstructShard>(&self, shards: &mut [T]) -> Result<(), Error>" in src
+    # the slot types helyim passes (Option<Vec<u8>>) and upstream's (buffer, flag) pairs
+    assert "impl ReconstructShard for Option<Vec<u8>>" in src
+    assert "ReconstructShard for (T, bool)" in src
+    # the old borrowed-slice form would not accept `bufs.as_mut()` by value
+    assert "encode<T: AsMut<[u8]>>(&self, shards: &mut [T])" not in src
+
+
+def test_reconstruct_batch_checks_every_stripe_length_first():
+    """hec_rs_reconstruct_batch reads exactly
+    total_shard_count entries per stripe, so the safe wrapper refuses a stripe
+    of any other length before it builds the pointer arrays."""
+    src = _wrapper_src()
+    body = src[src.index("pub fn reconstruct_batch"):]
+    body = body[:body.index("sys::hec_rs_reconstruct_batch")]
+    check = body.index("st.len() < n")
+    assert "Error::TooFewShards, j" in body and "Error::TooManyShards, j" in body
+    assert check < body.index("ptrs.push")

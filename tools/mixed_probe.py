@@ -32,8 +32,13 @@ def main():
     ap.add_argument("--uniform", type=int, default=0,
                     help="E > 0: every stripe 1 MiB with exactly E random erasures (the bench batch through "
                          "the ragged kernels; compare with the strided kernels' times)")
+    ap.add_argument("--fixed-len", type=int, default=0,
+                    help="> 0: every stripe this shard length, erasures still 0..4 mixed (separates the length mix)")
+    ap.add_argument("--fixed-e", type=int, default=-1,
+                    help=">= 0: every stripe exactly this many erasures, lengths still mixed (separates the e mix)")
     ap.add_argument("--pads", default="0", help="gap after every shard, one layout per value")
     ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes), per round")
+    ap.add_argument("--enc-remaps", default="1", help="ragged encode XCD remap (hec_set_ragged_encode_remap), per round")
     ap.add_argument("--strided", action="store_true",
                     help="with --uniform: also time the strided kernels on the same bytes each round")
     args = ap.parse_args()
@@ -50,6 +55,10 @@ def main():
     if args.uniform:
         Ls = np.full(n, 1 << 20)
         es = np.full(n, args.uniform)
+    if args.fixed_len > 0:
+        Ls = np.full(n, args.fixed_len)
+    if args.fixed_e >= 0:
+        es = np.full(n, args.fixed_e)
     full = (1 << 14) - 1
     masks = [full & ~int(sum(1 << int(i) for i in rng.choice(14, int(e), replace=False))) for e in es]
     pads = [int(x) for x in args.pads.split(",")]
@@ -65,6 +74,9 @@ def main():
     darr = {p: np.array(lays[p][0], dtype=B.desc_dtype()) for p in pads}  # converted once, not per call
     dev = torch.empty(max(o for _, o in lays.values()), dtype=torch.uint8, device="cuda")
     for s, (o, st, L, _) in enumerate(lays[pads[0]][0]):
+        if st == L:  # packed: the 10 data shards are one run
+            B.fill_splitmix(dev[o:o + 10 * L].view(1, 1, -1), 10 * L, bench.rank_seed_base(0) + s)
+            continue
         for i in range(10):
             B.fill_splitmix(dev[o + i * st:o + i * st + L].view(1, 1, -1), L, bench.rank_seed_base(0) + 14 * s + i)
     descs = lays[pads[0]][0]
@@ -74,11 +86,13 @@ def main():
         B.reconstruct_ragged(rs, dev, lays[p][0])
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
-    kinds = ["ragged"] + (["strided"] if args.strided and args.uniform else [])
+    kinds = ["ragged"] + (["strided"] if args.strided and (args.uniform or args.fixed_len) else [])
     mask_t = torch.tensor(masks, dtype=torch.int32, device="cuda")
-    for r, p, dv, kind in ((r, p, int(dv), k) for r in range(args.rounds) for p in pads
-                           for dv in args.decvecs.split(",") for k in kinds):
+    for r, p, dv, er, kind in ((r, p, int(dv), int(er), k) for r in range(args.rounds) for p in pads
+                               for dv in args.decvecs.split(",") for er in args.enc_remaps.split(",")
+                               for k in kinds):
         H.lib.hec_set_decode_vector_bytes(dv)
+        H.lib.hec_set_ragged_encode_remap(er)
         descs = lays[p][0]
         L0 = int(Ls[0])
         view = dev.as_strided((n, 14, L0), (14 * (L0 + p), L0 + p, 1))
@@ -102,13 +116,15 @@ def main():
         enc_b = sum(14 * d[2] for d in descs)
         dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
-                          "kind": kind, "pad": p, "dec_vec_bytes": dv, "round": r,
+                          "fixed_len": args.fixed_len, "fixed_e": args.fixed_e,
+                          "kind": kind, "pad": p, "dec_vec_bytes": dv, "enc_remap": er, "round": r,
                           "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
                           "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),
                           "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3),
                           "enc_bytes": int(enc_b), "dec_bytes": int(dec_b)}), flush=True)
     H.lib.hec_set_decode_vector_bytes(8)
+    H.lib.hec_set_ragged_encode_remap(1)
     descs = lays[pads[0]][0]
     if args.grouped:
         del dev

@@ -58,14 +58,23 @@ class HostBuffer:
     ``close()`` frees at once and must come after the views are gone."""
 
     def __init__(self, nbytes: int):
-        import numpy as np
         p = ctypes.c_void_p()
         check(lib.hec_host_alloc(nbytes, ctypes.byref(p)))
         self._ptr = p.value
         self.nbytes = nbytes
-        raw = (ctypes.c_uint8 * nbytes).from_address(self._ptr)
-        raw._owner = self  # numpy / torch views keep raw, raw keeps the owner alive
-        self.array = np.ctypeslib.as_array(raw)
+
+    @property
+    def array(self):
+        """A fresh numpy view. The view holds this object (through the ctypes
+        array under it) and this object holds no view, so there is no cycle:
+        the buffer is freed by refcount as soon as the last view and the
+        HostBuffer itself are gone."""
+        import numpy as np
+        if not self._ptr:
+            raise ValueError("HostBuffer is closed")
+        raw = (ctypes.c_uint8 * self.nbytes).from_address(self._ptr)
+        raw._owner = self
+        return np.ctypeslib.as_array(raw)
 
     @property
     def ptr(self) -> int:
@@ -83,7 +92,6 @@ class HostBuffer:
 
     def close(self) -> None:
         if self._ptr:
-            self.array = None
             check(lib.hec_host_free(self._ptr))
             self._ptr = None
 

@@ -80,3 +80,59 @@ def test_host_batch_from_numa_local_buffer():
     assert np.array_equal(t.numpy(), good)
     del t
     buf.close()
+
+
+_FALLBACK_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch
+import helyim_amd as H, helyim_amd.batch as B
+from oracle import corc
+torch.cuda.set_device(0)
+S, L = 4, 65536
+buf = H.HostBuffer(S * 14 * L)          # pinned_alloc with the NUMA-bound attempt failing
+t = buf.tensor((S, 14, L))
+t[:, :10] = torch.from_numpy(np.random.default_rng(9).integers(0, 256, (S, 10, L), dtype=np.uint8))
+rs = H.ReedSolomon(10, 4)
+B.host_encode_batch(rs, t)              # zero copy on the fallback buffer
+u = torch.zeros((S, 14, L), dtype=torch.uint8)  # pageable: pinned staging slots, also fallback-allocated
+u[:, :10] = t[:, :10]
+B.host_encode_batch(rs, u)
+ref = corc.encode_stripes(t[:, :10].numpy().copy())
+assert np.array_equal(t[:, 10:].numpy(), ref) and np.array_equal(u[:, 10:].numpy(), ref)
+print("fallback ok")
+"""
+
+
+def test_numa_bound_allocation_falls_back_to_any_node():
+    """NUMA placement is speed only. With the bound attempt forced
+    to fail (HEC_TEST_NUMA_BIND_FAIL=1, numa.cpp), every pinned buffer libhec
+    allocates -- hec_host_alloc and the pipelines' staging -- comes from the
+    default policy instead of failing, and the host batches stay bit-exact."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HEC_TEST_NUMA_BIND_FAIL="1")
+    p = subprocess.run([sys.executable, "-c", _FALLBACK_CHILD, root], env=env, capture_output=True, text=True,
+                       timeout=110, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "fallback ok" in p.stdout
+
+
+def test_host_buffer_views_keep_the_buffer_alive():
+    """a view of a HostBuffer holds the buffer, so dropping the
+    HostBuffer object while a view lives does not free the pinned memory."""
+    import gc
+    import weakref
+    import helyim_amd as H
+    buf = H.HostBuffer(1 << 20)
+    ref = weakref.ref(buf)
+    t = buf.tensor((1024, 1024))
+    del buf
+    gc.collect()
+    assert ref() is not None  # still owned by the view
+    t[:] = 7                   # writes land in live pinned memory
+    assert int(t.sum()) == 7 * (1 << 20)
+    del t
+    gc.collect()
+    assert ref() is None       # freed once the last view is gone

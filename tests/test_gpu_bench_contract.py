@@ -46,3 +46,16 @@ def test_bench_line_contract():
     assert 0 < pk["encode_frac"] < 1 and 0 < pk["decode_frac"] < 1
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0 and cb["sample"]
+
+
+@pytest.mark.gpu
+def test_bench_multi_gpu_host_leg_child():
+    """The bench's in-process multi-GPU end-to-end leg (run in a child
+    process when more than one GPU is visible) rehearsed on one GPU with the
+    device list 0,0: one host call split over two concurrent ranges."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--e2e-multi-child", "0,0"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["devices"] == [0, 0] and d["stripes"] == 512
+    assert d["encode_data_GiB_s"] > 1 and d["decode_data_GiB_s"] > 1

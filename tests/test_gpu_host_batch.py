@@ -183,3 +183,30 @@ def test_host_batch_multi_device_errors(gpu):
     B.host_encode_batch(rs, t, devices=[0, 0, 0])
     B.host_encode_batch(rs, u)
     assert torch.equal(t, u)
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3)])
+def test_host_batch_multi_device_generic_geometry(gpu, k, m):
+    """The multi-device split on geometries other than RS(10,4) (each range
+    takes the generic kernels), against the C oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rng = np.random.default_rng(7 * k + m)
+    n, S, L = k + m, 5, 4096 + 9
+    rs, ors = H.ReedSolomon(k, m), corc.CReedSolomon(k, m)
+    t = torch.zeros((S, n, L), dtype=torch.uint8).pin_memory()
+    a = t.numpy()
+    a[:, :k] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    want = a.copy()
+    for s in range(S):
+        ors.encode([want[s, i] for i in range(n)])
+    B.host_encode_batch(rs, t, devices=[0, 0, 0])
+    assert np.array_equal(a, want)
+    masks = np.full(S, (1 << n) - 1, np.uint32)
+    for s in range(S):
+        for i in rng.choice(n, int(rng.integers(1, m + 1)), replace=False):
+            masks[s] &= ~np.uint32(1 << int(i))
+            a[s, int(i)] = 0x3C
+    assert B.host_reconstruct_batch(rs, t, masks, devices=[0, 0]) == 0
+    assert np.array_equal(a, want)

@@ -39,6 +39,10 @@ def main():
     ap.add_argument("--pads", default="0", help="gap after every shard, one layout per value")
     ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes), per round")
     ap.add_argument("--enc-remaps", default="1", help="ragged encode XCD remap (hec_set_ragged_encode_remap), per round")
+    ap.add_argument("--orders", default="given",
+                    help="descriptor order of the ragged calls, per round: given (stripe order) or dealt "
+                         "(each erasure count's stripes split into 8 parts of equal workgroup counts, part x of "
+                         "every count placed in the x-th eighth of the map, so the 8 XCDs get equal decode work)")
     ap.add_argument("--strided", action="store_true",
                     help="with --uniform: also time the strided kernels on the same bytes each round")
     args = ap.parse_args()
@@ -71,7 +75,25 @@ def main():
         return descs, off
 
     lays = {p: layout(p) for p in pads}
-    darr = {p: np.array(lays[p][0], dtype=B.desc_dtype()) for p in pads}  # converted once, not per call
+
+    def dealt_order():
+        parts = [[] for _ in range(8)]
+        zero = []
+        for e in range(1, 15):
+            idx = [s for s in range(n) if bin(masks[s]).count("1") == 14 - e]
+            if not idx:
+                continue
+            w = np.array([(int(Ls[s]) + 4095) // 4096 for s in idx], dtype=np.int64)
+            start = np.cumsum(w) - w
+            for s, b in zip(idx, start):
+                parts[min(7, int(8 * b // w.sum()))].append(s)
+        zero = [s for s in range(n) if masks[s] == full]
+        return [s for part in parts for s in part] + zero
+
+    orders = args.orders.split(",")
+    perm = {"given": list(range(n)), "dealt": dealt_order() if "dealt" in orders else None}
+    # converted once, not per call
+    darr = {(p, o): np.array([lays[p][0][s] for s in perm[o]], dtype=B.desc_dtype()) for p in pads for o in orders}
     dev = torch.empty(max(o for _, o in lays.values()), dtype=torch.uint8, device="cuda")
     for s, (o, st, L, _) in enumerate(lays[pads[0]][0]):
         if st == L:  # packed: the 10 data shards are one run
@@ -88,9 +110,9 @@ def main():
     st = torch.cuda.current_stream()
     kinds = ["ragged"] + (["strided"] if args.strided and (args.uniform or args.fixed_len) else [])
     mask_t = torch.tensor(masks, dtype=torch.int32, device="cuda")
-    for r, p, dv, er, kind in ((r, p, int(dv), int(er), k) for r in range(args.rounds) for p in pads
-                               for dv in args.decvecs.split(",") for er in args.enc_remaps.split(",")
-                               for k in kinds):
+    for r, p, dv, er, kind, order in ((r, p, int(dv), int(er), k, o) for r in range(args.rounds) for p in pads
+                                      for dv in args.decvecs.split(",") for er in args.enc_remaps.split(",")
+                                      for k in kinds for o in (orders if k == "ragged" else ["given"])):
         H.lib.hec_set_decode_vector_bytes(dv)
         H.lib.hec_set_ragged_encode_remap(er)
         descs = lays[p][0]
@@ -100,12 +122,12 @@ def main():
         ev[0].record(st)
         for i in range(args.reps):
             if kind == "ragged":
-                B.encode_ragged(rs, dev, darr[p])
+                B.encode_ragged(rs, dev, darr[p, order])
             else:
                 B.encode_batch(rs, view)
             ev[2 * i + 1].record(st)
             if kind == "ragged":
-                B.reconstruct_ragged(rs, dev, darr[p])
+                B.reconstruct_ragged(rs, dev, darr[p, order])
             else:
                 B.reconstruct_batch(rs, view, mask_t)
             ev[2 * i + 2].record(st)
@@ -117,7 +139,7 @@ def main():
         dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
                           "fixed_len": args.fixed_len, "fixed_e": args.fixed_e,
-                          "kind": kind, "pad": p, "dec_vec_bytes": dv, "enc_remap": er, "round": r,
+                          "kind": kind, "order": order, "pad": p, "dec_vec_bytes": dv, "enc_remap": er, "round": r,
                           "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
                           "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),

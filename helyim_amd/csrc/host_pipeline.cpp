@@ -171,19 +171,26 @@ int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
     std::vector<std::string> details(R);
     std::vector<std::thread> th;
     th.reserve(R);
-    for (size_t r = 0; r < R; ++r) {
-        const uint32_t s0 = uint32_t(uint64_t(n_stripes) * r / R);
-        const uint32_t s1 = uint32_t(uint64_t(n_stripes) * (r + 1) / R);
-        th.emplace_back([&, r, s0, s1] {
-            const hipError_t e = hipSetDevice(devices[r]);
-            if (e != hipSuccess) {
-                rcs[r] = hip_fail(e, "hipSetDevice");
-            } else {
-                (void)hec_bind_thread_to_device(devices[r], nullptr);  // placement only: no-op when unknown
-                rcs[r] = fn(s0, s1 - s0, r);
-            }
-            if (rcs[r]) details[r] = hec_last_error_detail();
-        });
+    try {
+        for (size_t r = 0; r < R; ++r) {
+            const uint32_t s0 = uint32_t(uint64_t(n_stripes) * r / R);
+            const uint32_t s1 = uint32_t(uint64_t(n_stripes) * (r + 1) / R);
+            th.emplace_back([&, r, s0, s1] {
+                const hipError_t e = hipSetDevice(devices[r]);
+                if (e != hipSuccess) {
+                    rcs[r] = hip_fail(e, "hipSetDevice");
+                } else {
+                    (void)hec_bind_thread_to_device(devices[r], nullptr);  // placement only: no-op when unknown
+                    rcs[r] = fn(s0, s1 - s0, r);
+                }
+                if (rcs[r]) details[r] = hec_last_error_detail();
+            });
+        }
+    } catch (const std::exception& ex) {  // no thread for a range: nothing escapes the C ABI
+        for (size_t r = th.size(); r < R; ++r) {
+            rcs[r] = HEC_ERR_OUT_OF_MEMORY;
+            details[r] = std::string("no host thread for the range: ") + ex.what();
+        }
     }
     for (auto& t : th) t.join();
     for (size_t r = 0; r < R; ++r)

@@ -92,8 +92,24 @@ def main():
 
     orders = args.orders.split(",")
     perm = {"given": list(range(n)), "dealt": dealt_order() if "dealt" in orders else None}
+    # "eK": stripe order, every stripe with exactly K random erasures instead
+    # (the same bytes and lengths: separates the erasure mix from the rest)
+    emask = {}
+    for o in orders:
+        if o.startswith("e") and o[1:].isdigit():
+            er = np.random.default_rng(0xE0 + int(o[1:]))
+            emask[o] = [full & ~int(sum(1 << int(i) for i in er.choice(14, int(o[1:]), replace=False)))
+                        for _ in range(n)]
+            perm[o] = list(range(n))
+
+    def variant(p, o):
+        ds = [lays[p][0][s] for s in perm[o]]
+        if o in emask:
+            ds = [(d[0], d[1], d[2], emask[o][s]) for s, d in zip(perm[o], ds)]
+        return ds
     # converted once, not per call
-    darr = {(p, o): np.array([lays[p][0][s] for s in perm[o]], dtype=B.desc_dtype()) for p in pads for o in orders}
+    vdescs = {(p, o): variant(p, o) for p in pads for o in orders}
+    darr = {k: np.array(v, dtype=B.desc_dtype()) for k, v in vdescs.items()}
     dev = torch.empty(max(o for _, o in lays.values()), dtype=torch.uint8, device="cuda")
     for s, (o, st, L, _) in enumerate(lays[pads[0]][0]):
         if st == L:  # packed: the 10 data shards are one run
@@ -136,10 +152,13 @@ def main():
         dec = np.median([ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)])
         wall = ev[0].elapsed_time(ev[-1]) / args.reps
         enc_b = sum(14 * d[2] for d in descs)
+        if kind == "ragged":
+            descs = vdescs[p, order]
         dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
                           "fixed_len": args.fixed_len, "fixed_e": args.fixed_e,
-                          "kind": kind, "order": order, "pad": p, "dec_vec_bytes": dv, "enc_remap": er, "round": r,
+                          "kind": kind, "order": order, "pad": p, "dec_vec_bytes": dv, "enc_remap": er,
+                          "round": r,
                           "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
                           "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),

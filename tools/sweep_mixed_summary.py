@@ -57,7 +57,8 @@ def main():
                 continue
             j = json.loads(x)
             key = ("grouped_strided",) if j.get("grouped_strided") else (
-                j.get("kind", "ragged"), j.get("order", "given"), j.get("pad", 0), j.get("enc_remap", 0),
+                j.get("kind", "ragged"), j.get("order", "given"), "bal%d" % j.get("balance", 0), j.get("pad", 0),
+                j.get("enc_remap", 0),
                 j.get("dec_vec_bytes", 8))
             groups.setdefault(key, []).append(j)
         for key, js in groups.items():

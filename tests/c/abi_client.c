@@ -7,7 +7,9 @@
  *                        with a device status (HEC_ERR_NO_DEVICE / HEC_ERR_HIP)
  *   abi_client gpu D  -- bit-exact parity with the oracle: encode/verify over
  *                        ragged lengths, reconstruct / reconstruct_data of every
- *                        1..4-erasure pattern, the batched degraded read, and
+ *                        1..4-erasure pattern, the batched degraded read, one
+ *                        host batch split over a repeated device list
+ *                        (pageable and hec_host_alloc'd), and
  *                        write_ec_files / rebuild_ec_files in directory D.
  * Exit status 0 = all checks passed; prints one line per failed check. */
 #include <stdint.h>
@@ -186,6 +188,65 @@ static void check_batch(hec_rs_t* rs, void* ors) {
     }
 }
 
+/* hec_host_*_batch_multi: one [S][14][L] host batch split over the device
+ * list {0,0,0} (three concurrent ranges on one GPU, each on its own host
+ * thread and pipeline; an 8-GPU server lists 0..7), once in pageable memory
+ * (pooled pinned staging) and once in hec_host_alloc'd memory (zero copy);
+ * parity and a 0..5-erasure reconstruct against the C oracle. */
+static void check_host_batch_multi(void* ors) {
+    enum { S = 11 };
+    const size_t L = 65536 + 5, stripe = (size_t)N * L;
+    const int devs[3] = {0, 0, 0};
+    hec_rs_t* rs = NULL;
+    CHECK(hec_rs_new(K, M, &rs) == HEC_OK, "new");
+    for (int pinned = 0; pinned < 2; ++pinned) {
+        uint8_t* h = NULL;
+        if (pinned) CHECK(hec_host_alloc(S * stripe, (void**)&h) == HEC_OK && h, "host_alloc");
+        else h = malloc(S * stripe);
+        if (!h) return;
+        uint8_t* want = malloc(S * stripe);
+        for (int s = 0; s < S; ++s) {
+            uint8_t* p[N];
+            for (int i = 0; i < N; ++i) p[i] = want + s * stripe + i * L;
+            for (int i = 0; i < K; ++i) orc_splitmix64_fill(7000 + 31 * s + i, p[i], L);
+            orc_encode(ors, p, L, 0);
+        }
+        memcpy(h, want, S * stripe);
+        for (int s = 0; s < S; ++s) memset(h + s * stripe + K * L, 0xEE, M * L);
+        CHECK(hec_host_encode_batch_multi(rs, devs, 3, h, stripe, L, h + K * L, stripe, L, L, S) == HEC_OK,
+              "encode_multi (pinned %d)", pinned);
+        CHECK(memcmp(h, want, S * stripe) == 0, "encode_multi bytes (pinned %d)", pinned);
+        uint32_t masks[S];
+        for (int s = 0; s < S; ++s) {
+            masks[s] = 0x3FFFu;
+            for (int e = 0; e < s % 6; ++e) {  /* s % 6 erasures: 5 = too few present */
+                const int i = (3 * s + 5 * e) % N;
+                masks[s] &= ~(1u << i);
+                memset(h + s * stripe + i * L, 0xA5, L);
+            }
+        }
+        uint32_t bad = 99;
+        CHECK(hec_host_reconstruct_batch_multi(rs, devs, 2, h, stripe, L, L, S, masks, &bad) == HEC_OK,
+              "reconstruct_multi (pinned %d)", pinned);
+        int want_bad = 0;
+        for (int s = 0; s < S; ++s) {
+            if (__builtin_popcount(masks[s]) < K) {
+                ++want_bad;
+                continue;
+            }
+            CHECK(memcmp(h + s * stripe, want + s * stripe, stripe) == 0, "reconstruct_multi stripe %d", s);
+        }
+        CHECK(bad == (uint32_t)want_bad, "bad stripes %u, want %d", bad, want_bad);
+        const int bad_dev[2] = {0, 1 << 20};
+        CHECK(hec_host_encode_batch_multi(rs, bad_dev, 2, h, stripe, L, h + K * L, stripe, L, L, S) ==
+                  HEC_ERR_INVALID_ARGUMENT, "device out of range");
+        if (pinned) hec_host_free(h);
+        else free(h);
+        free(want);
+    }
+    hec_rs_free(rs);
+}
+
 /* The call shape INTEGRATION.md §3 gives the degraded read
  * (helyim-store/src/erasure_coding/mod.rs:403-491): one needle read spans
  * several intervals, each on a shard that is gone; the reader fans in the
@@ -318,6 +379,7 @@ int main(int argc, char** argv) {
     for (size_t j = 0; j < sizeof lens / sizeof lens[0]; ++j) check_encode_reconstruct(rs, ors, lens[j], 100 * j);
     check_batch(rs, ors);
     check_degraded_read_shape(rs, ors);
+    check_host_batch_multi(ors);
     check_files(argv[2]);
     orc_rs_free(ors);
     hec_rs_free(rs);

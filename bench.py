@@ -411,6 +411,7 @@ def mixed_section(rs, rank: int, n_stripes: int = 2048, e2e_stripes: int = 512) 
     w1 = time.time()
     t_e2e = w1 - w0
     groups.clear()
+    h = m = None  # no view of the pinned buffers outlives them
     for hb in bufs:
         hb.close()
     return {"stripes": n_stripes, "shard_lens": "64 KiB..4 MiB log-uniform", "erasures": "0..4 uniform",

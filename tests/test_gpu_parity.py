@@ -919,13 +919,22 @@ def test_randomised_device_batches_vs_oracle(gpu):
 def test_randomised_ragged_batches_vs_oracle(gpu):
     """Seeded sweep over ragged device batches: per-stripe lengths (all 8 KiB
     multiples -> bit-sliced ragged encode, or mixed -> table kernel), padded
-    strides and gaps, 0..5 erasures per stripe (5 = skipped and counted)."""
+    strides and gaps, 0..5 erasures per stripe (5 = skipped and counted); the
+    ragged encode's XCD remap on (default) and off (every third case)."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rng = np.random.default_rng(1016)
     rs = H.ReedSolomon(10, 4)
+    try:
+        _ragged_sweep(H, B, torch, rng, rs)
+    finally:
+        H.lib.hec_set_ragged_encode_remap(1)
+
+
+def _ragged_sweep(H, B, torch, rng, rs):
     for case in range(40):
+        assert H.lib.hec_set_ragged_encode_remap(0 if case % 3 == 0 else 1) == 0
         n = int(rng.integers(1, 25))
         if case % 2:
             lens = [8192 * int(rng.integers(1, 9)) for _ in range(n)]

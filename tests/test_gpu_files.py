@@ -226,3 +226,64 @@ def test_production_geometry_multi_slice_multi_job_vs_oracle(gpu, tmp_path):
         os.remove(a + H.to_ext(i))
     assert H.rebuild_ec_files(a) == [0, 1, 5, 9]
     assert [_file_digest(a + H.to_ext(i)) for i in range(14)] == want
+
+
+def _same_file(a, b, chunk=1 << 28):
+    """Byte-compare two files in 256 MiB pieces (numpy), sizes first."""
+    if os.path.getsize(a) != os.path.getsize(b):
+        return False
+    with open(a, "rb") as fa, open(b, "rb") as fb:
+        while True:
+            x, y = fa.read(chunk), fb.read(chunk)
+            if x != y:
+                return False
+            if not x:
+                return True
+
+
+@pytest.mark.parametrize("extra", [0, 4097])
+def test_reference_geometry_large_row_threshold(gpu, extra):
+    """The reference's own constants (1 GiB large blocks, 1 MiB small blocks,
+    256 KiB buffers) at the large-row threshold, encoder.rs:215 (`remaining >
+    large_block_size * DATA_SHARDS_COUNT`, strict): a .dat of exactly 10 GiB
+    takes NO large row (1024 small rows, 1 GiB shard files); 10 GiB + 4097 B
+    takes one large row (each data shard's 1 GiB block in 64 slices of 16 MiB)
+    and one zero-padded small row (1 GiB + 1 MiB shard files). Every shard file
+    is byte-compared with the C oracle's encoder.rs restatement, then four
+    shards (two data, two parity) are rebuilt on both sides and compared.
+    Files live in /dev/shm (~40 GB at the peak, removed afterwards)."""
+    import shutil
+    import tempfile
+    import helyim_amd as H
+    from oracle import corc
+    GiB, MiB = 1 << 30, 1 << 20
+    size = 10 * GiB + extra
+    d = tempfile.mkdtemp(prefix="hec_refgeom_", dir="/dev/shm")
+    try:
+        a, b = os.path.join(d, "a"), os.path.join(d, "b")
+        with open(a + ".dat", "wb") as f:
+            left, part = size, 0
+            while left:
+                n = min(left, GiB)
+                f.write(memoryview(corc.splitmix64_bytes(0x5EED7000 + part, n)))
+                left -= n
+                part += 1
+        os.link(a + ".dat", b + ".dat")  # one copy of the 10 GiB input, read by both encoders
+        H.write_ec_files(a)
+        assert corc.write_ec_files(b) == 0
+        want_len = GiB + (MiB if extra else 0)
+        for i in range(14):
+            assert os.path.getsize(a + H.to_ext(i)) == want_len, i
+            assert _same_file(a + H.to_ext(i), b + O.to_ext(i)), i
+        os.remove(a + ".dat")
+        os.remove(b + ".dat")
+        drop = [3, 9, 10, 12]
+        for i in drop:
+            os.remove(a + H.to_ext(i))
+            os.remove(b + O.to_ext(i))
+        assert H.rebuild_ec_files(a) == drop
+        assert corc.rebuild_ec_files(b) == (0, drop)
+        for i in drop:
+            assert _same_file(a + H.to_ext(i), b + O.to_ext(i)), i
+    finally:
+        shutil.rmtree(d, ignore_errors=True)

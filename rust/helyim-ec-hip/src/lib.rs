@@ -248,6 +248,54 @@ impl<T: AsRef<[u8]> + AsMut<[u8]>> ReconstructShard for (T, bool) {
     }
 }
 
+impl ReedSolomon {
+    /// Stripe count of a packed `[S][total][L]` host batch, or the upstream
+    /// error a wrong size maps to.
+    fn packed_stripes(&self, bytes: usize, shard_len: usize) -> Result<u32, Error> {
+        let stripe = self.total_shard_count().checked_mul(shard_len).ok_or(Error::IncorrectShardSize)?;
+        if shard_len == 0 {
+            return Err(Error::EmptyShard);
+        }
+        if bytes % stripe != 0 {
+            return Err(Error::IncorrectShardSize);
+        }
+        u32::try_from(bytes / stripe).map_err(|_| Error::TooManyShards)
+    }
+
+    /// One packed host batch `[S][total][L]` (parity written in place into
+    /// shards data..total of every stripe), split into contiguous stripe
+    /// ranges over `devices` (`hec_host_encode_batch_multi`; a device may
+    /// repeat). Pinned memory (`hec_host_alloc`) is coded zero-copy.
+    pub fn encode_batch_multi(&self, devices: &[i32], stripes: &mut [u8], shard_len: usize) -> Result<(), Error> {
+        let s = self.packed_stripes(stripes.len(), shard_len)?;
+        let (n, k, l) = (self.total_shard_count() as u64, self.data_shard_count() as u64, shard_len as u64);
+        let base = stripes.as_mut_ptr();
+        check(unsafe {
+            sys::hec_host_encode_batch_multi(self.0, devices.as_ptr(), devices.len(), base, n * l, l,
+                                             base.add((k * l) as usize), n * l, l, l, s)
+        })
+    }
+
+    /// In-place reconstruct of a packed `[S][total][L]` host batch over
+    /// `devices` (`hec_host_reconstruct_batch_multi`); `present_masks[s]` bit i
+    /// = shard i of stripe s present. Returns the stripes skipped for too few
+    /// present shards.
+    pub fn reconstruct_batch_multi(&self, devices: &[i32], stripes: &mut [u8], shard_len: usize,
+                                   present_masks: &[u32]) -> Result<u32, Error> {
+        let s = self.packed_stripes(stripes.len(), shard_len)?;
+        if present_masks.len() != s as usize {
+            return Err(Error::InvalidShardFlags);
+        }
+        let (n, l) = (self.total_shard_count() as u64, shard_len as u64);
+        let mut bad = 0u32;
+        check(unsafe {
+            sys::hec_host_reconstruct_batch_multi(self.0, devices.as_ptr(), devices.len(), stripes.as_mut_ptr(),
+                                                  n * l, l, l, s, present_masks.as_ptr(), &mut bad)
+        })?;
+        Ok(bad)
+    }
+}
+
 impl Drop for ReedSolomon {
     fn drop(&mut self) {
         unsafe { sys::hec_rs_free(self.0) }

@@ -90,3 +90,15 @@ def test_reconstruct_batch_checks_every_stripe_length_first():
     check = body.index("st.len() < n")
     assert "Error::TooFewShards, j" in body and "Error::TooManyShards, j" in body
     assert check < body.index("ptrs.push")
+
+
+def test_wrapper_exposes_the_multi_device_host_batches():
+    """The safe wrapper carries the in-process multi-GPU host path (round 3):
+    packed [S][14][L] batches, sizes checked before the unsafe call."""
+    src = _squash(_wrapper_src())
+    assert "pub fn encode_batch_multi(&self, devices: &[i32], stripes: &mut [u8], shard_len: usize)" in src
+    assert "pub fn reconstruct_batch_multi(&self, devices: &[i32], stripes: &mut [u8], shard_len: usize," in src
+    enc = src[src.index("pub fn encode_batch_multi"):]
+    assert enc.index("packed_stripes") < enc.index("sys::hec_host_encode_batch_multi")
+    rec = src[src.index("pub fn reconstruct_batch_multi"):]
+    assert rec.index("present_masks.len() != s as usize") < rec.index("sys::hec_host_reconstruct_batch_multi")

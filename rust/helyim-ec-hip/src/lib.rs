@@ -272,7 +272,7 @@ impl ReedSolomon {
         let base = stripes.as_mut_ptr();
         check(unsafe {
             sys::hec_host_encode_batch_multi(self.0, devices.as_ptr(), devices.len(), base, n * l, l,
-                                             base.add((k * l) as usize), n * l, l, l, s)
+                                             base.wrapping_add((k * l) as usize), n * l, l, l, s)
         })
     }
 

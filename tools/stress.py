@@ -3,7 +3,8 @@ immutable contexts, per-device mutex-guarded state, reentrant calls).
 
 Worker threads run, for --seconds, a random mix of:
   * per-call ReedSolomon encode / reconstruct (staged and direct sizes),
-  * host batches (pinned zero-copy and pageable pooled staging),
+  * host batches (pinned zero-copy and pageable pooled staging), half of
+    them split over a repeated device list (hec_host_*_batch_multi),
   * the batched ragged reconstruct (hec_rs_reconstruct_batch),
   * file-level write_ec_files / rebuild_ec_files on small volumes,
   * device batches on a private torch stream,
@@ -69,7 +70,8 @@ def main():
             t = t.pin_memory()
         a = t.numpy()
         a[:, :10] = rng.integers(0, 256, (S, 10, L), dtype=np.uint8)
-        B.host_encode_batch(rs, t)
+        devs = [0] * int(rng.integers(1, 4)) if rng.integers(0, 2) else None
+        B.host_encode_batch(rs, t, devices=devs)
         assert np.array_equal(a[:, 10:], corc.encode_stripes(np.ascontiguousarray(a[:, :10]))), "host encode"
         want = a.copy()
         masks = np.full(S, 0x3FFF, np.uint32)
@@ -77,9 +79,9 @@ def main():
             for i in rng.choice(14, int(rng.integers(0, 5)), replace=False):
                 masks[s] &= ~np.uint32(1 << int(i))
                 a[s, int(i)] = 0x11
-        assert B.host_reconstruct_batch(rs, t, masks) == 0
+        assert B.host_reconstruct_batch(rs, t, masks, devices=devs) == 0
         assert np.array_equal(a, want), "host reconstruct"
-        note("host_batch")
+        note("host_batch" if devs is None else "host_batch_multi")
 
     def ragged(rng):
         n = int(rng.integers(1, 20))

@@ -166,6 +166,10 @@ int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
             return fail(HEC_ERR_INVALID_ARGUMENT,
                         "device " + std::to_string(devices[r]) + " of " + std::to_string(count) + " in the list");
     if (n_stripes == 0) return HEC_OK;
+    // The process-wide host worker pool starts on its first use and its
+    // threads inherit that thread's CPU affinity: start it here, from the
+    // caller's thread, not from a range thread bound to one GPU's node.
+    pool_run(0, 1, [](size_t) {});
     const size_t R = std::min<size_t>(n_devices, n_stripes);
     std::vector<int> rcs(R, HEC_OK);
     std::vector<std::string> details(R);

@@ -98,7 +98,6 @@ SIGNATURES = {
     "hec_set_host_zero_copy": (_I, [_I]),
     "hec_set_xcd_parts": (_I, [_I]),
     "hec_set_chunk_rotation": (_I, [_I]),
-    "hec_set_xcd_phase": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
     "hec_device_count": (_I, [ctypes.POINTER(_I)]),
     "hec_set_device": (_I, [_I]),

@@ -675,11 +675,6 @@ int hec_set_xcd_parts(int parts) {
     return HEC_OK;
 }
 
-int hec_set_xcd_phase(int on) {
-    update_launch_config([&](LaunchConfig& c) { c.xcd_phase = on ? 1 : 0; });
-    return HEC_OK;
-}
-
 int hec_set_chunk_rotation(int on) {
     update_launch_config([&](LaunchConfig& c) { c.chunk_rot = on ? 1 : 0; });
     return HEC_OK;

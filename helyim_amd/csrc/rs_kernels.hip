@@ -393,16 +393,10 @@ __device__ __forceinline__ void fast_item(const ApplyArgs& a, uint32_t per_strip
         asm volatile("" ::"s"(a.in_base), "s"(a.in_stripe), "s"(a.in_shard), "s"(a.out_base), "s"(a.out_stripe),
                      "s"(a.out_shard), "s"(a.len), "s"(a.masks), "s"(a.lut), "s"(a.tabs), "s"(a.xcd_remap),
                      "s"(a.map_q8), "s"(a.map_r8), "s"(a.cps_mul), "s"(a.cps_shift), "s"(a.chunks_per_stripe),
-                     "s"(a.chunk_rot), "s"(a.xcd_phase));
+                     "s"(a.chunk_rot));
         if (a.xcd_remap) {  // XCD x = b % 8 takes the x-th eighth: x*q + min(x, r) + b/8
             const uint32_t x = b & 7u, q = a.map_q8, r = a.map_r8;
-            uint32_t j = b >> 3;
-            if (a.xcd_phase) {  // start x/8 of the way into the eighth, wrap around
-                const uint32_t qx = q + (x < r ? 1u : 0u);
-                j += (x * qx) >> 3;
-                if (j >= qx) j -= qx;
-            }
-            item = x * q + (x < r ? x : r) + j;
+            item = x * q + (x < r ? x : r) + (b >> 3);
         }
         stripe = fastdiv(item, a.cps_mul, a.cps_shift);
         chunk = item - stripe * per_stripe;
@@ -835,7 +829,6 @@ static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
-    a.xcd_phase = uint32_t(cfg.xcd_phase);
     a.chunk_rot = uint32_t(cfg.chunk_rot);
     set_fast_map(a, a.n_items, a.chunks_per_stripe);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
@@ -901,7 +894,6 @@ static hipError_t launch_rs104_tb(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
-    a.xcd_phase = uint32_t(cfg.xcd_phase);
     a.chunk_rot = uint32_t(cfg.chunk_rot);
     set_fast_map(a, a.n_items, a.chunks_per_stripe);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
@@ -924,7 +916,6 @@ static hipError_t launch_rs104_pair(ApplyArgs a, const LaunchConfig& cfg, hipStr
     if (a.n_items == 0) return hipSuccess;
     a.xcd_remap = uint32_t(cfg.xcd_remap);
     a.xcd_parts = uint32_t(cfg.xcd_parts);
-    a.xcd_phase = uint32_t(cfg.xcd_phase);
     a.chunk_rot = 0;  // the pair kernel has no rotated order
     set_fast_map(a, a.n_items / 2, a.chunks_per_stripe / 2);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
@@ -972,7 +963,6 @@ static hipError_t launch_rs104(const ApplyArgs& a, const Rs104Pick& pick, const 
         b.n_items = uint64_t(b.chunks_per_stripe) * a.n_stripes;
         if (b.n_items == 0) return hipSuccess;
         b.xcd_remap = uint32_t(cfg.xcd_remap);
-        b.xcd_phase = uint32_t(cfg.xcd_phase);
         b.chunk_rot = uint32_t(cfg.chunk_rot);
         set_fast_map(b, b.n_items, b.chunks_per_stripe);
         const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;

@@ -49,7 +49,6 @@ struct ApplyArgs {
     uint32_t* bad_count;         // optional: stripes skipped for too few present shards
     uint32_t xcd_remap;          // 1: workgroups sharing an XCD take consecutive chunks
     uint32_t xcd_parts;          // with xcd_remap 1: regions per XCD worked on concurrently
-    uint32_t xcd_phase;          // with xcd_remap 1: XCD x starts x/8 into its region (measurement)
     uint32_t chunk_rot;          // 1: rotate each stripe's chunk order by a hash of the stripe id
     uint32_t fast104;            // 1: RS(10,4) plan set with 4-row tables; encode = plan 0 at
                                  //    offset 0, decode = tables at lut[mask] * 200 words
@@ -112,7 +111,6 @@ struct LaunchConfig {
     int xcd_remap = 1;           // 0 none, 1 eighths, G>=2 runs of G chunks per XCD (speed only)
     int blocks_per_cu = 0;       // >0: cap resident workgroups per CU via dynamic LDS (0 = no cap)
     int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
-    int xcd_phase = 0;           // with xcd_remap 1: 1 = XCD x starts x/8 of the way into its eighth (speed only)
     int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
     int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
     int dec_vec_bytes = 8;       // RS(10,4) decode bytes per lane per shard: 8 (default: dwordx2, 2 KiB

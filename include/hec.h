@@ -388,11 +388,6 @@ int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, in
 /* With xcd_remap 1: the workgroups of one XCD work on `parts` regions of the
  * batch concurrently (1 = one contiguous eighth per XCD). Speed only. */
 int hec_set_xcd_parts(int parts);
-/* With xcd_remap 1: 1 = XCD x starts x/8 of the way into its eighth of the
- * batch (wrapping), so the 8 XCDs never stream addresses a whole number of
- * eighths apart at the same time; 0 = each starts at its eighth's beginning
- * (default). Speed only. */
-int hec_set_xcd_phase(int on);
 /* 1: each stripe walks its 4 KiB chunks starting at a hashed offset, so
  * concurrently running stripes touch different column ranges. Speed only. */
 int hec_set_chunk_rotation(int on);

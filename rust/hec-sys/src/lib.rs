@@ -187,7 +187,6 @@ extern "C" {
                                  blocks_per_cu: c_int) -> c_int;
     pub fn hec_set_xcd_parts(parts: c_int) -> c_int;
     pub fn hec_set_chunk_rotation(on: c_int) -> c_int;
-    pub fn hec_set_xcd_phase(on: c_int) -> c_int;
     pub fn hec_set_kernel_mode(mode: c_int) -> c_int;
     pub fn hec_set_workgroup_size(threads: c_int) -> c_int;
     pub fn hec_set_decode_vector_bytes(bytes: c_int) -> c_int;

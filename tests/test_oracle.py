@@ -247,3 +247,72 @@ def test_c_oracle_file_layer_small_geometry(tmp_path, size):
     O.write_ec_files(b, 16, 640, 32)
     for i in range(14):
         assert open(a + O.to_ext(i), "rb").read() == open(b + O.to_ext(i), "rb").read()
+
+
+# ---- a third formulation: polynomial interpolation over GF(2^8) -------------
+# The construction V x inv(V[0..k]) with V[r][c] = r^c is
+# the systematic evaluation code: shard r of a stripe is p(r) for the unique
+# polynomial p of degree < k with p(i) = data_i at i = 0..k-1. Lagrange
+# interpolation restates that without a matrix inverse (pure-Python GF
+# arithmetic from log/exp tables built here, not the oracle's), so encode and
+# reconstruct of both oracles are checked against a formulation that shares
+# no code with them.
+def _gf():
+    exp, log = [0] * 512, [0] * 256
+    x = 1
+    for i in range(255):
+        exp[i] = x
+        log[x] = i
+        x <<= 1
+        if x & 0x100:
+            x ^= 0x11D
+    for i in range(255, 512):
+        exp[i] = exp[i - 255]
+    mul = lambda a, b: 0 if a == 0 or b == 0 else exp[log[a] + log[b]]  # noqa: E731
+    inv = lambda a: exp[255 - log[a]]  # noqa: E731
+    return mul, inv
+
+
+def _lagrange_eval(xs, ys, x0, mul, inv):
+    """p(x0) for the polynomial through (xs[i], ys[i]); addition is XOR."""
+    acc = 0
+    for i, xi in enumerate(xs):
+        num, den = 1, 1
+        for j, xj in enumerate(xs):
+            if j != i:
+                num = mul(num, x0 ^ xj)
+                den = mul(den, xi ^ xj)
+        acc ^= mul(ys[i], mul(num, inv(den)))
+    return acc
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (3, 2)])
+def test_encode_and_reconstruct_match_interpolation(k, m):
+    mul, inv = _gf()
+    rng = np.random.default_rng(100 * k + m)
+    L = 9
+    data = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    want = np.zeros((k + m, L), np.uint8)
+    want[:k] = data
+    for col in range(L):
+        for r in range(k, k + m):
+            want[r, col] = _lagrange_eval(list(range(k)), [int(v) for v in data[:, col]], r, mul, inv)
+    # both oracles' encode
+    rs = O.ReedSolomon(k, m)
+    sh = [data[i].copy() for i in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+    rs.encode(sh)
+    assert np.array_equal(np.stack(sh), want)
+    csh = [data[i].copy() for i in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+    corc.CReedSolomon(k, m).encode(csh)
+    assert np.array_equal(np.stack(csh), want)
+    # any k surviving shards determine p: interpolate the lost ones back
+    for _ in range(6):
+        lost = sorted(int(i) for i in rng.choice(k + m, m, replace=False))
+        alive = [i for i in range(k + m) if i not in lost][:k]
+        for col in range(L):
+            for r in lost:
+                v = _lagrange_eval(alive, [int(want[i, col]) for i in alive], r, mul, inv)
+                assert v == want[r, col]
+        got = [None if i in lost else want[i].copy() for i in range(k + m)]
+        rs.reconstruct(got)
+        assert np.array_equal(np.stack(got), want), lost

@@ -156,9 +156,12 @@ uint32_t chunk_stripes(uint64_t shard_len, int n, uint32_t n_stripes) {
 // staging on that node). A device listed twice runs two ranges concurrently on
 // two pipelines. Every range runs to its end; the call returns the status of
 // the first failing range in list order (its detail prefixed with the range).
+constexpr size_t kMaxDeviceRanges = 256;
 int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
                       const std::function<int(uint32_t s0, uint32_t count, size_t range)>& fn) {
     if (!devices || n_devices == 0) return fail(HEC_ERR_INVALID_ARGUMENT, "empty device list");
+    if (n_devices > kMaxDeviceRanges)  // one host thread per entry
+        return fail(HEC_ERR_INVALID_ARGUMENT, "more than " + std::to_string(kMaxDeviceRanges) + " device entries");
     int count = 0;
     HEC_TRY(hec_device_count(&count));
     for (size_t r = 0; r < n_devices; ++r)

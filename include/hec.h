@@ -221,7 +221,7 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
  * failing range in list order (hec_last_error_detail names the range).
  * Arguments and results otherwise as the single-device calls;
  * *n_bad_stripes is the sum over ranges. An empty list or a device out of
- * range -> HEC_ERR_INVALID_ARGUMENT before any work. */
+ * range, or more than 256 entries -> HEC_ERR_INVALID_ARGUMENT before any work. */
 int hec_host_encode_batch_multi(const hec_rs_t* rs, const int* devices, size_t n_devices,
                                 const uint8_t* h_data, uint64_t data_stripe_stride, uint64_t data_shard_stride,
                                 uint8_t* h_parity, uint64_t parity_stripe_stride, uint64_t parity_shard_stride,

@@ -199,6 +199,8 @@ def test_strided_batch_geometry_checked_before_device():
         assert lib.hec_host_encode_batch_multi(rs.handle, devs, 2, *args) == 66, args
     assert lib.hec_host_reconstruct_batch_multi(rs.handle, devs, 2, P, 14 * L, L - 1, L, 2, masks, None) == 66
     assert lib.hec_host_encode_batch_multi(rs.handle, None, 0, P, 14 * L, L, P, 14 * L, L, L, 2) != 0
+    many = (ctypes.c_int * 257)()
+    assert lib.hec_host_encode_batch_multi(rs.handle, many, 257, P, 14 * L, L, P, 14 * L, L, L, 2) == 66
 
 
 def test_kernel_name_follows_dispatch_under_every_knob():

@@ -102,3 +102,40 @@ def test_wrapper_exposes_the_multi_device_host_batches():
     assert enc.index("packed_stripes") < enc.index("sys::hec_host_encode_batch_multi")
     rec = src[src.index("pub fn reconstruct_batch_multi"):]
     assert rec.index("present_masks.len() != s as usize") < rec.index("sys::hec_host_reconstruct_batch_multi")
+
+
+def _call_args(src, start):
+    """Top-level arguments of the call whose '(' is at src[start]."""
+    depth, args, cur, i = 0, [], "", start
+    while True:
+        ch = src[i]
+        if ch in "([{":
+            depth += 1
+            if depth > 1:
+                cur += ch
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                if cur.strip():
+                    args.append(cur.strip())
+                return args
+            cur += ch
+        elif ch == "," and depth == 1:
+            args.append(cur.strip())
+            cur = ""
+        elif depth >= 1:
+            cur += ch
+        i += 1
+
+
+def test_wrapper_calls_match_extern_arity():
+    """Every `sys::hec_*(...)` call in the safe wrapper passes as many
+    arguments as the extern block declares (no compiler here checks it)."""
+    decl = _rust_decls()
+    src = _wrapper_src()
+    src = re.sub(r"//[^\n]*", "", src)
+    calls = [(m.group(1), _call_args(src, m.end() - 1)) for m in re.finditer(r"sys::(hec_\w+)\(", src)]
+    assert len(calls) >= 15
+    for name, args in calls:
+        assert name in decl, name
+        assert len(args) == decl[name], (name, len(args), decl[name], args)

@@ -40,6 +40,7 @@ _I = ctypes.c_int
 SIGNATURES = {
     "hec_strerror": (ctypes.c_char_p, [_I]),
     "hec_last_error_detail": (ctypes.c_char_p, []),
+    "hec_last_error_values": (_I, [ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_I)]),
     "hec_rs_new": (_I, [_S, _S, ctypes.POINTER(_P)]),
     "hec_rs_free": (None, [_P]),
     "hec_rs_data_shard_count": (_S, [_P]),
@@ -123,3 +124,10 @@ def strerror(code: int) -> str:
 
 def last_detail() -> str:
     return lib.hec_last_error_detail().decode()
+
+
+def last_values() -> tuple:
+    """(a, b, os_errno) of the last failure on this thread (hec_last_error_values)."""
+    a, b, e = _U64(), _U64(), _I()
+    lib.hec_last_error_values(ctypes.byref(a), ctypes.byref(b), ctypes.byref(e))
+    return a.value, b.value, e.value

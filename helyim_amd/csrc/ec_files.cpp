@@ -71,17 +71,24 @@ struct ErrorSlot {
     std::mutex mu;
     std::atomic<int> code{HEC_OK};
     std::string detail;
-    void set(int c, const std::string& d) {
+    ErrorValues values;  // hec_last_error_values of the first failure
+    void set(int c, const std::string& d, const ErrorValues& v = ErrorValues{}) {
         std::lock_guard<std::mutex> lk(mu);
         if (code.load() == HEC_OK) {
             detail = d;
+            values = v;
             code.store(c);
         }
     }
     bool failed() const { return code.load() != HEC_OK; }
 };
 
-void io_error(ErrorSlot& e, const std::string& what) { e.set(HEC_ERR_IO, what + ": " + std::strerror(errno)); }
+void io_error(ErrorSlot& e, const std::string& what) {
+    const int err = errno;
+    ErrorValues v;
+    v.os_errno = err;
+    e.set(HEC_ERR_IO, what + ": " + std::strerror(err), v);
+}
 
 // ---------------------------------------------------------------------------
 // Small fixed thread pool with fork/join task groups.
@@ -283,7 +290,7 @@ class FilePipeline {
         int rc = gpu(s, job);
         clk_.submit_ns += StageClock::now() - t2;
         if (rc) {
-            err_.set(rc, hec_last_error_detail());
+            err_.set(rc, hec_last_error_detail(), last_error_values());
             return release(si);
         }
         {
@@ -307,9 +314,11 @@ class FilePipeline {
         clk_.reset();
         int code = err_.code.load();
         std::string detail = err_.detail;
+        const ErrorValues values = err_.values;
         err_.code.store(HEC_OK);
         err_.detail.clear();
-        return code ? fail(code, detail) : HEC_OK;
+        err_.values = ErrorValues{};
+        return code ? fail_with(code, detail, values) : HEC_OK;
     }
     ErrorSlot& errors() { return err_; }
 
@@ -456,7 +465,7 @@ int open_outputs(const std::string& base, const bool* which, Fd* out) {
     for (auto& t : th) t.join();
     for (int i = 0; i < N; ++i)
         if (which[i] && out[i].fd < 0)
-            return fail(HEC_ERR_IO, "open " + shard_name(base, i) + ": " + std::strerror(err[i]));
+            return fail_errno(HEC_ERR_IO, "open " + shard_name(base, i), err[i]);
     return HEC_OK;
 }
 
@@ -474,9 +483,9 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     // generate_ec_files: open .dat read-only (encoder.rs:58-62)
     Fd dat;
     dat.fd = ::open((base + ".dat").c_str(), O_RDONLY);
-    if (dat.fd < 0) return fail(HEC_ERR_IO, "open " + base + ".dat: " + std::strerror(errno));
+    if (dat.fd < 0) return fail_errno(HEC_ERR_IO, "open " + base + ".dat", errno);
     struct stat st;
-    if (::fstat(dat.fd, &st) != 0) return fail(HEC_ERR_IO, std::string("stat .dat: ") + std::strerror(errno));
+    if (::fstat(dat.fd, &st) != 0) return fail_errno(HEC_ERR_IO, "stat .dat", errno);
     int64_t remaining = int64_t(st.st_size);
 
     Rs104 rs;  // ReedSolomon::new(10, 4) (encoder.rs:208-209)
@@ -494,8 +503,9 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     // the reference checks block % buf at the first row of each kind (encoder.rs:139-144)
     const bool has_large = remaining > int64_t(large_row);
     if (has_large && large % buf_size != 0)
-        return fail(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
-                    "unexpected block size " + std::to_string(large) + ", buffer size " + std::to_string(buf_size));
+        return fail_values(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
+                           "unexpected block size " + std::to_string(large) + ", buffer size " + std::to_string(buf_size),
+                           large, buf_size);
     // rows of each kind, to size the staging buffers no larger than needed
     const uint64_t n_large = has_large ? (uint64_t(remaining) - 1) / large_row : 0;
     const int64_t small_bytes = remaining - int64_t(n_large * large_row);
@@ -547,8 +557,9 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     if (remaining > 0 && small % buf_size != 0 && !pipe.errors().failed()) {
         int frc = pipe.drain();
         if (frc) return frc;
-        return fail(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
-                    "unexpected block size " + std::to_string(small) + ", buffer size " + std::to_string(buf_size));
+        return fail_values(HEC_ERR_UNEXPECTED_BLOCK_SIZE,
+                           "unexpected block size " + std::to_string(small) + ", buffer size " + std::to_string(buf_size),
+                           small, buf_size);
     }
     while (remaining > 0 && !pipe.errors().failed()) {
         const uint64_t rows_left = (uint64_t(remaining) + small_row - 1) / small_row;
@@ -588,12 +599,12 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
         if (::stat(name.c_str(), &st) == 0) {
             has[i] = true;
             in[i].fd = ::open(name.c_str(), O_RDONLY);
-            if (in[i].fd < 0) return fail(HEC_ERR_IO, "open " + name + ": " + std::strerror(errno));
+            if (in[i].fd < 0) return fail_errno(HEC_ERR_IO, "open " + name, errno);
         } else {
-            if (errno != ENOENT) return fail(HEC_ERR_IO, "stat " + name + ": " + std::strerror(errno));
+            if (errno != ENOENT) return fail_errno(HEC_ERR_IO, "stat " + name, errno);
             has[i] = false;
             out[i].fd = ::open(name.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-            if (out[i].fd < 0) return fail(HEC_ERR_IO, "open " + name + ": " + std::strerror(errno));
+            if (out[i].fd < 0) return fail_errno(HEC_ERR_IO, "open " + name, errno);
             rebuilt.push_back(uint32_t(i));
         }
     }
@@ -613,13 +624,14 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
         if (!has[i]) continue;
         ++npresent;
         struct stat st;
-        if (::fstat(in[i].fd, &st) != 0) return fail(HEC_ERR_IO, std::string("stat shard: ") + std::strerror(errno));
+        if (::fstat(in[i].fd, &st) != 0) return fail_errno(HEC_ERR_IO, "stat shard", errno);
         size[i] = uint64_t(st.st_size);
     }
     uint64_t row_size = 0;  // input_buffer_data_size
     uint64_t rows = 0;
     int end_rc = HEC_OK;
     std::string end_detail;
+    uint64_t end_expected = 0, end_actual = 0;  // UnexpectedEcShardSize(expected, actual)
     for (;;) {
         const uint64_t start = rows * (row_size ? row_size : 1);
         bool stop = false;
@@ -635,6 +647,8 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
                 end_rc = HEC_ERR_UNEXPECTED_EC_SHARD_SIZE;
                 end_detail = "ec shard size expected " + std::to_string(row_size) + " but actually is " +
                              std::to_string(n);
+                end_expected = row_size;
+                end_actual = n;
             }
         }
         if (stop || end_rc != HEC_OK) break;
@@ -693,7 +707,7 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
         }
         if ((rc = pipe.drain())) return rc;
     }
-    if (end_rc != HEC_OK) return fail(end_rc, end_detail);
+    if (end_rc != HEC_OK) return fail_values(end_rc, end_detail, end_expected, end_actual);
     if (n_ids) *n_ids = rebuilt.size();
     if (ids)
         for (size_t i = 0; i < rebuilt.size(); ++i) ids[i] = rebuilt[i];

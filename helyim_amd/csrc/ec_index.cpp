@@ -26,7 +26,7 @@ namespace {
 
 constexpr uint64_t kEntry = 16;  // NEEDLE_ENTRY_SIZE: u64 id, u32 offset/8, i32 size, big endian
 
-int io(const std::string& what) { return fail(HEC_ERR_IO, what + ": " + std::strerror(errno)); }
+int io(const std::string& what) { return fail_errno(HEC_ERR_IO, what, errno); }
 int eof(const std::string& what) { return fail(HEC_ERR_IO, what + ": failed to fill whole buffer"); }
 
 struct File {

@@ -33,7 +33,7 @@ constexpr uint64_t kDataShards = 10;  // DATA_SHARDS_COUNT
 constexpr int kTotalShards = 14;
 constexpr uint64_t kEntry = 16;  // NEEDLE_ENTRY_SIZE
 
-int io(const std::string& what) { return fail(HEC_ERR_IO, what + ": " + std::strerror(errno)); }
+int io(const std::string& what) { return fail_errno(HEC_ERR_IO, what, errno); }
 
 uint64_t be64(const uint8_t* p) {
     uint64_t v = 0;
@@ -488,7 +488,7 @@ int hec_ec_volume_open_ex(const char* base_filename, uint64_t large_block_size, 
     int rc = v->ecx.open(v->base, true);
     if (rc) return rc;
     v->ecj_fd = ::open((v->base + ".ecj").c_str(), O_RDWR | O_CREAT, 0644);
-    if (v->ecj_fd < 0) return fail(HEC_ERR_IO, "open " + v->base + ".ecj: " + std::strerror(errno));
+    if (v->ecj_fd < 0) return fail_errno(HEC_ERR_IO, "open " + v->base + ".ecj", errno);
     // .vif: load the version, or write the default VolumeInfo (version 2)
     bool found = false;
     uint32_t ver = 0;

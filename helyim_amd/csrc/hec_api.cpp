@@ -19,16 +19,41 @@
 namespace hec {
 
 static thread_local std::string g_detail;
+static thread_local ErrorValues g_values;
 
-void set_detail(const std::string& s) { g_detail = s; }
+void set_detail(const std::string& s) {
+    g_detail = s;
+    g_values = ErrorValues{};
+}
 
 int fail(int code, const std::string& detail) {
-    g_detail = detail;
+    set_detail(detail);
     return code;
 }
 
+int fail_values(int code, const std::string& detail, uint64_t a, uint64_t b) {
+    set_detail(detail);
+    g_values.a = a;
+    g_values.b = b;
+    return code;
+}
+
+int fail_errno(int code, const std::string& what, int err) {
+    set_detail(what + ": " + std::strerror(err));
+    g_values.os_errno = err;
+    return code;
+}
+
+int fail_with(int code, const std::string& detail, const ErrorValues& v) {
+    g_detail = detail;
+    g_values = v;
+    return code;
+}
+
+ErrorValues last_error_values() { return g_values; }
+
 int hip_fail(hipError_t e, const char* what) {
-    g_detail = std::string(what) + ": " + hipGetErrorString(e);
+    set_detail(std::string(what) + ": " + hipGetErrorString(e));
     if (e == hipErrorOutOfMemory) return HEC_ERR_OUT_OF_MEMORY;
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return HEC_ERR_NO_DEVICE;
     return HEC_ERR_HIP;
@@ -622,6 +647,13 @@ const char* hec_strerror(int status) {
 }
 
 const char* hec_last_error_detail(void) { return g_detail.c_str(); }
+
+int hec_last_error_values(uint64_t* a, uint64_t* b, int* os_errno) {
+    if (a) *a = g_values.a;
+    if (b) *b = g_values.b;
+    if (os_errno) *os_errno = g_values.os_errno;
+    return HEC_OK;
+}
 
 const char* hec_version(void) { return "libhec 0.1.0 (gfx950)"; }
 

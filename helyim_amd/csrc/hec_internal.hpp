@@ -24,9 +24,22 @@ struct hec_rs {
 
 namespace hec {
 
-// Thread-local failure detail (hec_last_error_detail).
+// Thread-local failure detail (hec_last_error_detail) and the payload of the
+// failure (hec_last_error_values): helyim's EcShardError variants carry
+// (usize, usize) or an io::Error (helyim-ec/src/errors.rs:55-66), which the C
+// ABI's status code alone cannot rebuild.
+struct ErrorValues {
+    uint64_t a = 0, b = 0;  // UnexpectedEcShardSize(expected, actual), UnexpectedBlockSize(block, buf), Underflow
+    int os_errno = 0;       // errno behind an HEC_ERR_IO (0: no OS error, e.g. a short read)
+};
 void set_detail(const std::string& s);
-int fail(int code, const std::string& detail);
+int fail(int code, const std::string& detail);  // clears the values
+int fail_values(int code, const std::string& detail, uint64_t a, uint64_t b);
+// detail = what + ": " + strerror(err), os_errno = err
+int fail_errno(int code, const std::string& what, int err);
+// Re-raise a failure captured on another thread with its values.
+int fail_with(int code, const std::string& detail, const ErrorValues& v);
+ErrorValues last_error_values();
 
 // Strided-batch geometry sanity (the C ABI sees only pointers, so sizes cannot
 // be checked): shards of a stripe and stripes of a shard must not overlap,

@@ -176,6 +176,7 @@ int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
     const size_t R = std::min<size_t>(n_devices, n_stripes);
     std::vector<int> rcs(R, HEC_OK);
     std::vector<std::string> details(R);
+    std::vector<ErrorValues> values(R);
     std::vector<std::thread> th;
     th.reserve(R);
     try {
@@ -190,7 +191,10 @@ int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
                     (void)hec_bind_thread_to_device(devices[r], nullptr);  // placement only: no-op when unknown
                     rcs[r] = fn(s0, s1 - s0, r);
                 }
-                if (rcs[r]) details[r] = hec_last_error_detail();
+                if (rcs[r]) {
+                    details[r] = hec_last_error_detail();
+                    values[r] = last_error_values();
+                }
             });
         }
     } catch (const std::exception& ex) {  // no thread for a range: nothing escapes the C ABI
@@ -204,8 +208,10 @@ int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
         if (rcs[r]) {
             const uint32_t s0 = uint32_t(uint64_t(n_stripes) * r / R);
             const uint32_t s1 = uint32_t(uint64_t(n_stripes) * (r + 1) / R);
-            return fail(rcs[r], "device " + std::to_string(devices[r]) + " stripes [" + std::to_string(s0) + ", " +
-                                    std::to_string(s1) + "): " + details[r]);
+            return fail_with(rcs[r],
+                             "device " + std::to_string(devices[r]) + " stripes [" + std::to_string(s0) + ", " +
+                                 std::to_string(s1) + "): " + details[r],
+                             values[r]);
         }
     return HEC_OK;
 }

@@ -40,10 +40,62 @@ class EcShardError(Exception):
     code = -1
 
 
-class Io(EcShardError): code = 32
-class Underflow(EcShardError): code = 33
-class UnexpectedEcShardSize(EcShardError): code = 34
-class UnexpectedBlockSize(EcShardError): code = 35
+class Io(EcShardError):
+    """EcShardError::Io(std::io::Error): ``errno`` is the OS error behind it
+    (hec_last_error_values; 0 when there was none, e.g. a short read), and
+    ``os_error`` the matching OSError (None without an errno)."""
+    code = 32
+
+    def __init__(self, detail: str, errno: int = 0):
+        import os as _os
+        self.detail, self.errno = detail, errno
+        self.os_error = OSError(errno, _os.strerror(errno)) if errno else None
+        # thiserror "Io error: {0}" over io::Error's Display "... (os error N)"
+        super().__init__(f"Io error: {detail}" + (f" (os error {errno})" if errno else ""))
+
+
+class _SizePair(EcShardError):
+    """The (usize, usize) variants of EcShardError (errors.rs:60-65); str() is
+    helyim's thiserror text with the two values filled in."""
+    fmt = ""
+
+    def __init__(self, a: int, b: int):
+        self.values = (a, b)
+        super().__init__(self.fmt.format(a, b))
+
+
+class Underflow(_SizePair):
+    """Underflow(found, required); helyim's format prints {0} twice (errors.rs:60)."""
+    code = 33
+    fmt = "Only {0} shards found but {0} required"
+
+
+class UnexpectedEcShardSize(_SizePair):
+    """UnexpectedEcShardSize(expected, actual) (encoder.rs:276-279)."""
+    code = 34
+    fmt = "ec shard size expected {0} but actually is {1}"
+
+    @property
+    def expected(self) -> int:
+        return self.values[0]
+
+    @property
+    def actual(self) -> int:
+        return self.values[1]
+
+
+class UnexpectedBlockSize(_SizePair):
+    """UnexpectedBlockSize(block_size, buf_size) (encoder.rs:140-143)."""
+    code = 35
+    fmt = "unexpected block size {0}, buffer size {1}"
+
+    @property
+    def block_size(self) -> int:
+        return self.values[0]
+
+    @property
+    def buf_size(self) -> int:
+        return self.values[1]
 
 
 class EcVolumeError(Exception):
@@ -93,7 +145,13 @@ def check(code: int) -> None:
     if code in _RS:
         raise _RS[code](_lib.strerror(code))
     if code in _EC:
-        raise _EC[code](_message(code))
+        cls = _EC[code]
+        a, b, errno = _lib.last_values()
+        if issubclass(cls, _SizePair):
+            raise cls(a, b)
+        if cls is Io:
+            raise Io(_lib.last_detail() or _lib.strerror(code), errno)
+        raise cls(_message(code))
     raise DeviceError(code, _message(code))
 
 

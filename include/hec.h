@@ -69,6 +69,17 @@ const char* hec_strerror(int status);
 /* Thread-local detail of the last failure on this thread (e.g. the errno text,
  * the two sizes of UnexpectedEcShardSize). Empty string when none. */
 const char* hec_last_error_detail(void);
+/* Payload of the last failure on this thread, so a binding can rebuild the
+ * reference's error values (helyim-ec/src/errors.rs:55-66), not only its
+ * variant: *a / *b = the two usizes of UnexpectedEcShardSize(expected, actual)
+ * (encoder.rs:276-279) and UnexpectedBlockSize(block_size, buf_size)
+ * (encoder.rs:140-143); *os_errno = the errno behind an HEC_ERR_IO (the
+ * io::Error of EcShardError::Io, encoder.rs:175 -- 0 when the failure had no OS
+ * error, e.g. a short read). Meaningful right after a call returned one of
+ * codes 32..35 (every such return sets all three; 0 where the variant has no
+ * such value); other statuses may leave stale values. Null pointers are
+ * skipped. Returns HEC_OK. */
+int hec_last_error_values(uint64_t* a, uint64_t* b, int* os_errno);
 
 /* ---- device selection (no reference counterpart: helyim has no GPU) -------
  * Every entry point works on the calling thread's current HIP device. A

@@ -74,6 +74,7 @@ pub const HEC_SMALL_BLOCK_SIZE: u64 = 1024 * 1024;
 extern "C" {
     pub fn hec_strerror(status: c_int) -> *const c_char;
     pub fn hec_last_error_detail() -> *const c_char;
+    pub fn hec_last_error_values(a: *mut u64, b: *mut u64, os_errno: *mut c_int) -> c_int;
 
     // device selection (per calling thread)
     pub fn hec_device_count(count: *mut c_int) -> c_int;

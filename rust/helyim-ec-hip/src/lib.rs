@@ -3,21 +3,28 @@
 //! /root/reference/helyim-ec/src/encoder.rs:191,208-209,249-250,288 and
 //! helyim-store/src/erasure_coding/mod.rs:411-412,426), the batched degraded
 //! read, and `write_ec_files` / `rebuild_ec_files`
-//! (helyim-ec/src/encoder.rs:39-50). Swapping
-//! `use reed_solomon_erasure::{ReedSolomon, galois_8::Field}` for
-//! `use helyim_ec_hip::ReedSolomon` is the whole change at each call site.
+//! (helyim-ec/src/encoder.rs:39-50).
 //!
-//! `Error` has upstream's variants in upstream's order, so the codes map 1:1;
-//! inside helyim a maintainer would `pub use reed_solomon_erasure::Error` and
-//! keep `to_err`'s table.
+//! The swap in helyim: `use helyim_ec_hip::ReedSolomon`
+//! for `use reed_solomon_erasure::{ReedSolomon, galois_8::Field}` at each call
+//! site, and `#[from] helyim_ec_hip::Error` for `#[from]
+//! reed_solomon_erasure::Error` at helyim-ec/src/errors.rs:27,59. `Error` has
+//! upstream's 13 variants in upstream's order and Display text, plus
+//! `Device` for libhec's own failures (no GPU, HIP errors), which reaches gRPC
+//! as `Status::internal` through helyim's existing `From<..> for Status`
+//! impls (errors.rs:37-41, 68-72). `EcShardError` has helyim's exact shape
+//! (errors.rs:54-66), payloads included.
 
 use std::ffi::{CStr, CString};
+use std::fmt;
+use std::io;
 use std::os::raw::c_int;
 
 use hec_sys as sys;
 
-/// reed_solomon_erasure::Error, declaration order (codes 1..=13).
-#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+/// reed_solomon_erasure::Error, declaration order (codes 1..=13), plus
+/// libhec's device / argument failures (codes >= 64).
+#[derive(Clone, Debug, PartialEq, Eq)]
 pub enum Error {
     TooFewShards,
     TooManyShards,
@@ -32,17 +39,65 @@ pub enum Error {
     EmptyShard,
     InvalidShardFlags,
     InvalidIndex,
-    /// libhec device / argument failure (codes >= 64): no upstream variant.
-    Device(i32),
+    /// libhec device / argument failure: (status code, hec_last_error_detail).
+    /// No upstream variant; helyim maps it to `Status::internal` like the rest.
+    Device(i32, String),
 }
 
+impl fmt::Display for Error {
+    /// Upstream 6.0.0's Display text for the 13 variants (the same strings
+    /// `hec_strerror` returns for codes 1..=13).
+    fn fmt(&self, f: &mut fmt::Formatter<'_>) -> fmt::Result {
+        use Error::*;
+        let text = match self {
+            TooFewShards => "The number of provided shards is smaller than the one in codec",
+            TooManyShards => "The number of provided shards is greater than the one in codec",
+            TooFewDataShards => "The number of provided data shards is smaller than the one in codec",
+            TooManyDataShards => "The number of provided data shards is greater than the one in codec",
+            TooFewParityShards => "The number of provided parity shards is smaller than the one in codec",
+            TooManyParityShards => "The number of provided parity shards is greater than the one in codec",
+            TooFewBufferShards => "The number of provided buffer shards is smaller than the number of parity shards in codec",
+            TooManyBufferShards => "The number of provided buffer shards is greater than the number of parity shards in codec",
+            IncorrectShardSize => "At least one of the provided shards is not of the correct size",
+            TooFewShardsPresent => "The number of shards present is smaller than number of parity shards, cannot reconstruct missing shards",
+            EmptyShard => "The first shard provided is of zero length",
+            InvalidShardFlags => "The number of flags does not match the total number of shards",
+            InvalidIndex => "The data shard index provided is greater or equal to the number of data shards in codec",
+            Device(code, detail) => {
+                let what = unsafe { CStr::from_ptr(sys::hec_strerror(*code)) }.to_string_lossy();
+                return if detail.is_empty() {
+                    write!(f, "libhec error {code}: {what}")
+                } else {
+                    write!(f, "libhec error {code}: {what} ({detail})")
+                };
+            }
+        };
+        f.write_str(text)
+    }
+}
+
+impl std::error::Error for Error {}
+
+/// The variant of a status code (codes 1..=13 upstream's, anything else
+/// `Device` with this thread's failure detail).
 pub fn to_err(code: c_int) -> Error {
     use Error::*;
-    const RS: [Error; 13] = [TooFewShards, TooManyShards, TooFewDataShards, TooManyDataShards,
-                             TooFewParityShards, TooManyParityShards, TooFewBufferShards,
-                             TooManyBufferShards, IncorrectShardSize, TooFewShardsPresent, EmptyShard,
-                             InvalidShardFlags, InvalidIndex];
-    if (1..=13).contains(&code) { RS[(code - 1) as usize] } else { Device(code) }
+    match code {
+        1 => TooFewShards,
+        2 => TooManyShards,
+        3 => TooFewDataShards,
+        4 => TooManyDataShards,
+        5 => TooFewParityShards,
+        6 => TooManyParityShards,
+        7 => TooFewBufferShards,
+        8 => TooManyBufferShards,
+        9 => IncorrectShardSize,
+        10 => TooFewShardsPresent,
+        11 => EmptyShard,
+        12 => InvalidShardFlags,
+        13 => InvalidIndex,
+        c => Device(c, last_error_detail()),
+    }
 }
 
 fn check(code: c_int) -> Result<(), Error> {
@@ -52,6 +107,14 @@ fn check(code: c_int) -> Result<(), Error> {
 /// The text libhec gives for the last failure on this thread.
 pub fn last_error_detail() -> String {
     unsafe { CStr::from_ptr(sys::hec_last_error_detail()) }.to_string_lossy().into_owned()
+}
+
+/// (a, b, errno) of the last failure on this thread (`hec_last_error_values`):
+/// the two usizes of the size variants, the OS error behind an Io.
+pub fn last_error_values() -> (u64, u64, i32) {
+    let (mut a, mut b, mut e) = (0u64, 0u64, 0 as c_int);
+    unsafe { sys::hec_last_error_values(&mut a, &mut b, &mut e) };
+    (a, b, e)
 }
 
 pub struct ReedSolomon(*mut sys::hec_rs_t);
@@ -302,32 +365,70 @@ impl Drop for ReedSolomon {
     }
 }
 
-/// helyim_ec::EcShardError (helyim-ec/src/errors.rs:55-66), with libhec's
-/// device failures as their own variant.
+/// helyim_ec::EcShardError with helyim's exact variants and payloads
+/// (helyim-ec/src/errors.rs:54-66). libhec's device failures arrive as
+/// `ErasureCoding(Error::Device(..))`, so no variant is added.
 #[derive(Debug)]
 pub enum EcShardError {
-    Io(String),
+    Io(io::Error),
     ErasureCoding(Error),
-    Underflow(String),
-    UnexpectedEcShardSize(String),
-    UnexpectedBlockSize(String),
-    Device(i32, String),
+    Underflow(usize, usize),
+    UnexpectedEcShardSize(usize, usize),
+    UnexpectedBlockSize(usize, usize),
 }
 
+impl fmt::Display for EcShardError {
+    /// helyim's thiserror formats (errors.rs:56-65), Underflow's `{0}` twice included.
+    fn fmt(&self, f: &mut fmt::Formatter<'_>) -> fmt::Result {
+        match self {
+            EcShardError::Io(e) => write!(f, "Io error: {e}"),
+            EcShardError::ErasureCoding(e) => write!(f, "Erasure coding error: {e}"),
+            EcShardError::Underflow(a, _) => write!(f, "Only {a} shards found but {a} required"),
+            EcShardError::UnexpectedEcShardSize(a, b) => write!(f, "ec shard size expected {a} but actually is {b}"),
+            EcShardError::UnexpectedBlockSize(a, b) => write!(f, "unexpected block size {a}, buffer size {b}"),
+        }
+    }
+}
+
+impl std::error::Error for EcShardError {
+    fn source(&self) -> Option<&(dyn std::error::Error + 'static)> {
+        match self {
+            EcShardError::Io(e) => Some(e),
+            EcShardError::ErasureCoding(e) => Some(e),
+            _ => None,
+        }
+    }
+}
+
+impl From<io::Error> for EcShardError {
+    fn from(e: io::Error) -> Self {
+        EcShardError::Io(e)
+    }
+}
+
+impl From<Error> for EcShardError {
+    fn from(e: Error) -> Self {
+        EcShardError::ErasureCoding(e)
+    }
+}
+
+/// The EcShardError of a file-layer status, payload from
+/// `hec_last_error_values` (codes 32..=35; RS and device codes wrap as
+/// `ErasureCoding`, like errors.rs:58-59).
 fn file_err(code: c_int) -> EcShardError {
-    let d = last_error_detail();
+    let (a, b, errno) = last_error_values();
     match code {
-        sys::HEC_ERR_IO => EcShardError::Io(d),
-        sys::HEC_ERR_UNDERFLOW => EcShardError::Underflow(d),
-        sys::HEC_ERR_UNEXPECTED_EC_SHARD_SIZE => EcShardError::UnexpectedEcShardSize(d),
-        sys::HEC_ERR_UNEXPECTED_BLOCK_SIZE => EcShardError::UnexpectedBlockSize(d),
-        c if (1..=13).contains(&c) => EcShardError::ErasureCoding(to_err(c)),
-        c => EcShardError::Device(c, d),
+        sys::HEC_ERR_IO if errno != 0 => EcShardError::Io(io::Error::from_raw_os_error(errno)),
+        sys::HEC_ERR_IO => EcShardError::Io(io::Error::new(io::ErrorKind::Other, last_error_detail())),
+        sys::HEC_ERR_UNDERFLOW => EcShardError::Underflow(a as usize, b as usize),
+        sys::HEC_ERR_UNEXPECTED_EC_SHARD_SIZE => EcShardError::UnexpectedEcShardSize(a as usize, b as usize),
+        sys::HEC_ERR_UNEXPECTED_BLOCK_SIZE => EcShardError::UnexpectedBlockSize(a as usize, b as usize),
+        c => EcShardError::ErasureCoding(to_err(c)),
     }
 }
 
 fn cstr(s: &str) -> Result<CString, EcShardError> {
-    CString::new(s).map_err(|e| EcShardError::Io(e.to_string()))
+    CString::new(s).map_err(|e| EcShardError::Io(io::Error::new(io::ErrorKind::InvalidInput, e)))
 }
 
 /// helyim_ec::write_ec_files (encoder.rs:39-46): base.dat -> base.ec00..ec13.

@@ -10,8 +10,10 @@
  *                        1..4-erasure pattern, the batched degraded read, one
  *                        host batch split over a repeated device list
  *                        (pageable and hec_host_alloc'd), and
- *                        write_ec_files / rebuild_ec_files in directory D.
+ *                        write_ec_files / rebuild_ec_files in directory D, and
+ *                        helyim's EcShardError payloads (hec_last_error_values).
  * Exit status 0 = all checks passed; prints one line per failed check. */
+#define _POSIX_C_SOURCE 200809L /* truncate */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -365,8 +367,69 @@ static void check_files(const char* dir) {
     }
 }
 
+/* helyim's EcShardError payloads through hec_last_error_values
+ * (helyim-ec/src/errors.rs:55-66): Io's errno, UnexpectedBlockSize(block, buf)
+ * (encoder.rs:139-144) on the large-row and the small-row check, and -- with
+ * a device -- UnexpectedEcShardSize(expected, actual) (encoder.rs:272-280)
+ * from a rebuild whose third row is short after two rows were rebuilt. */
+static void check_values(int code, uint64_t want_a, uint64_t want_b, int want_errno, const char* what) {
+    uint64_t a = 7, b = 7;
+    int e = 7;
+    CHECK(hec_last_error_values(&a, &b, &e) == HEC_OK, "last_error_values");
+    CHECK(a == want_a && b == want_b && e == want_errno, "%s (code %d): values (%llu, %llu, errno %d), want (%llu, %llu, %d)",
+          what, code, (unsigned long long)a, (unsigned long long)b, e, (unsigned long long)want_a,
+          (unsigned long long)want_b, want_errno);
+}
+
+static void check_file_errors(const char* dir, int with_gpu) {
+    char base[4096], p[4200];
+    snprintf(base, sizeof base, "%s/missing", dir);
+    int rc = hec_write_ec_files(base);
+    CHECK(rc == HEC_ERR_IO, "write_ec_files(missing) = %d", rc);
+    check_values(rc, 0, 0, 2 /* ENOENT */, "missing .dat");
+
+    snprintf(base, sizeof base, "%s/blk", dir);
+    write_dat(base, 10 * 640 + 1); /* one large row (strict '>', encoder.rs:215) */
+    rc = hec_write_ec_files_ex(base, 24, 640, 32);
+    CHECK(rc == HEC_ERR_UNEXPECTED_BLOCK_SIZE, "large-row block size: %d", rc);
+    check_values(rc, 640, 24, 0, "large-row UnexpectedBlockSize");
+    if (!with_gpu) return;
+
+    write_dat(base, 100); /* small rows only: checked after the pipeline is set up */
+    rc = hec_write_ec_files_ex(base, 24, 640, 32);
+    CHECK(rc == HEC_ERR_UNEXPECTED_BLOCK_SIZE, "small-row block size: %d", rc);
+    check_values(rc, 32, 24, 0, "small-row UnexpectedBlockSize");
+
+    snprintf(base, sizeof base, "%s/trunc", dir);
+    write_dat(base, 25000000); /* 3 rows of 1 MiB blocks: shard files of 3 MiB */
+    CHECK(hec_write_ec_files(base) == HEC_OK, "write_ec_files(25 MB)");
+    uint8_t* want3;
+    size_t n3 = 0;
+    snprintf(p, sizeof p, "%s.ec03", base);
+    CHECK(read_file(p, &want3, &n3) == 0 && n3 == 3u << 20, "read ec03 (%zu)", n3);
+    unlink(p);
+    snprintf(p, sizeof p, "%s.ec00", base);
+    CHECK(truncate(p, (2 << 20) + 5) == 0, "truncate ec00");
+    uint32_t ids[N];
+    size_t n_ids = 0;
+    rc = hec_rebuild_ec_files(base, ids, &n_ids);
+    CHECK(rc == HEC_ERR_UNEXPECTED_EC_SHARD_SIZE, "rebuild of a truncated shard: %d", rc);
+    check_values(rc, 1u << 20, 5, 0, "UnexpectedEcShardSize");
+    /* the two full rows were rebuilt before the short one was read, as upstream */
+    uint8_t* got;
+    size_t ng = 0;
+    snprintf(p, sizeof p, "%s.ec03", base);
+    CHECK(read_file(p, &got, &ng) == 0 && ng == 2u << 20 && memcmp(got, want3, ng) == 0,
+          "rows rebuilt before the error (%zu bytes)", ng);
+    free(got);
+    free(want3);
+}
+
 int main(int argc, char** argv) {
-    if (argc >= 2 && strcmp(argv[1], "nogpu") == 0) return run_nogpu();
+    if (argc >= 2 && strcmp(argv[1], "nogpu") == 0) {
+        if (argc >= 3) check_file_errors(argv[2], 0);
+        return run_nogpu();
+    }
     if (argc < 3 || strcmp(argv[1], "gpu") != 0) {
         fprintf(stderr, "usage: %s nogpu | gpu <tmpdir>\n", argv[0]);
         return 2;
@@ -381,6 +444,7 @@ int main(int argc, char** argv) {
     check_degraded_read_shape(rs, ors);
     check_host_batch_multi(ors);
     check_files(argv[2]);
+    check_file_errors(argv[2], 1);
     orc_rs_free(ors);
     hec_rs_free(rs);
     printf("%s: %d failed checks\n", argv[0], g_fail);

@@ -114,9 +114,66 @@ def test_constants_and_ext():
 
 
 def test_file_layer_io_errors(tmp_path):
+    """EcShardError::Io carries the io::Error: the errno comes back through
+    hec_last_error_values (encoder.rs:58-62 opens the .dat with `?`)."""
+    import errno
+
     import helyim_amd as H
-    with pytest.raises(H.Io):
+    with pytest.raises(H.Io) as ei:
         H.write_ec_files(str(tmp_path / "missing"))
+    assert ei.value.errno == errno.ENOENT
+    assert isinstance(ei.value.os_error, FileNotFoundError)
+    assert str(ei.value).startswith("Io error: open ") and str(ei.value).endswith("(os error 2)")
+    # an unwritable output directory: the first shard file's open fails
+    ro = tmp_path / "ro"
+    ro.mkdir()
+    open(ro / "v.dat", "wb").write(b"x" * 100)
+    os.chmod(ro, 0o500)
+    try:
+        if os.access(ro, os.W_OK):  # root ignores the mode bits
+            pytest.skip("running as root: directory permissions are not enforced")
+        with pytest.raises(H.Io) as ei:
+            H.write_ec_files(str(ro / "v"))
+        assert ei.value.errno == errno.EACCES
+    finally:
+        os.chmod(ro, 0o700)
+
+
+def test_file_layer_size_errors_carry_helyims_values(tmp_path):
+    """UnexpectedBlockSize(block_size, buf_size) (encoder.rs:139-144) and
+    UnexpectedEcShardSize(expected, actual) (encoder.rs:272-280) come back with
+    both usizes (hec_last_error_values), checked before any device work: the
+    large-row block check precedes the first row, and a rebuild whose first
+    row already disagrees never reaches the GPU."""
+    import helyim_amd as H
+    from helyim_amd import _lib
+    base = str(tmp_path / "v")
+    open(base + ".dat", "wb").write(b"x" * (10 * 640 + 1))  # one large row (strict '>')
+    with pytest.raises(H.UnexpectedBlockSize) as ei:
+        H.generate_ec_files(base, 24, 640, 32)
+    assert ei.value.values == (640, 24) and (ei.value.block_size, ei.value.buf_size) == (640, 24)
+    assert str(ei.value) == "unexpected block size 640, buffer size 24"
+    assert _lib.last_values() == (640, 24, 0)
+
+    rb = str(tmp_path / "r")
+    for i in range(14):
+        if i != 2:
+            open(rb + H.to_ext(i), "wb").write(bytes(999 if i == 5 else 1000))
+    with pytest.raises(H.UnexpectedEcShardSize) as ei:
+        H.rebuild_ec_files(rb)
+    assert (ei.value.expected, ei.value.actual) == (1000, 999)
+    assert str(ei.value) == "ec shard size expected 1000 but actually is 999"
+    # a payload-free failure afterwards does not leak the old values into Io
+    with pytest.raises(H.Io) as ei:
+        H.write_ec_files(str(tmp_path / "missing"))
+    assert _lib.last_values() == (0, 0, 2)
+
+
+def test_underflow_display_mirrors_helyims_format():
+    """errors.rs:60 formats Underflow with {0} twice; the mirror keeps that."""
+    import helyim_amd as H
+    e = H.Underflow(3, 10)
+    assert e.values == (3, 10) and str(e) == "Only 3 shards found but 3 required"
 
 
 def test_reconstruct_batch_validation_before_device():

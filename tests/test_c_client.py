@@ -33,7 +33,7 @@ def test_c_client_without_device(tmp_path):
     if _gpu_present():
         pytest.skip("a GPU is present; the gpu-marked C client test covers this build")
     exe = _build(tmp_path)
-    r = subprocess.run([exe, "nogpu"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, "nogpu", str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
 
 

@@ -57,8 +57,11 @@ def test_unexpected_block_size(gpu, tmp_path):
     import helyim_amd as H
     base = str(tmp_path / "v")
     open(base + ".dat", "wb").write(b"x" * 100)
-    with pytest.raises(H.UnexpectedBlockSize):
+    with pytest.raises(H.UnexpectedBlockSize) as ei:
         H.generate_ec_files(base, 24, 640, 32)
+    # helyim's payload: UnexpectedBlockSize(block_size, buf_size), encoder.rs:140-143
+    assert (ei.value.block_size, ei.value.buf_size) == (32, 24)
+    assert str(ei.value) == "unexpected block size 32, buffer size 24"
 
 
 def test_rebuild_errors(gpu, tmp_path):
@@ -81,8 +84,10 @@ def test_rebuild_errors(gpu, tmp_path):
     os.remove(base + H.to_ext(3))
     with open(base + H.to_ext(0), "r+b") as f:
         f.truncate((1 << 20) + 5)
-    with pytest.raises(H.UnexpectedEcShardSize):
+    with pytest.raises(H.UnexpectedEcShardSize) as ei:
         H.rebuild_ec_files(base)
+    assert (ei.value.expected, ei.value.actual) == (1 << 20, 5)
+    assert str(ei.value) == "ec shard size expected 1048576 but actually is 5"
     assert _sha(base + H.to_ext(3)) == shas[3]
 
 

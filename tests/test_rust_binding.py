@@ -139,3 +139,77 @@ def test_wrapper_calls_match_extern_arity():
     for name, args in calls:
         assert name in decl, name
         assert len(args) == decl[name], (name, len(args), decl[name], args)
+
+
+def _enum_body(src, name):
+    start = src.index(f"pub enum {name} {{")
+    return src[start:src.index("\n}", start)]
+
+
+def _variants(src, name):
+    body = re.sub(r"//[^\n]*", "", _enum_body(src, name))
+    body = body[body.index("{") + 1:]
+    return [v.strip() for v in re.findall(r"\s*([A-Z]\w*(?:\([^)]*\))?),", body)]
+
+
+def test_error_types_have_helyims_shapes_and_traits():
+    """VERDICT r03 "next" 1: helyim's errors.rs wraps the RS error with
+    `#[error("Erasure coding error: {0}")] ErasureCoding(#[from] ..)` (:26-27,
+    :58-59), which needs Display + std::error::Error, and EcShardError's
+    variants carry (usize, usize) / std::io::Error (errors.rs:55-66)."""
+    src = _wrapper_src()
+    for ty in ("Error", "EcShardError"):
+        assert re.search(rf"impl fmt::Display for {ty} \{{", src), ty
+        assert re.search(rf"impl std::error::Error for {ty} \{{", src), ty
+    # helyim's EcShardError, variant for variant (errors.rs:55-66); device
+    # failures ride inside ErasureCoding(Error::Device(..)), no extra variant
+    assert _variants(src, "EcShardError") == [
+        "Io(io::Error)", "ErasureCoding(Error)", "Underflow(usize, usize)",
+        "UnexpectedEcShardSize(usize, usize)", "UnexpectedBlockSize(usize, usize)"]
+    assert "use std::io;" in src
+    # upstream's 13 variants in declaration order, then libhec's own
+    assert _variants(src, "Error") == [
+        "TooFewShards", "TooManyShards", "TooFewDataShards", "TooManyDataShards", "TooFewParityShards",
+        "TooManyParityShards", "TooFewBufferShards", "TooManyBufferShards", "IncorrectShardSize",
+        "TooFewShardsPresent", "EmptyShard", "InvalidShardFlags", "InvalidIndex", "Device(i32, String)"]
+    # the #[from] conversions helyim's `?` relies on
+    assert "impl From<io::Error> for EcShardError" in src and "impl From<Error> for EcShardError" in src
+
+
+def test_error_display_texts_match_upstream_and_helyim():
+    """Display of the 13 RS variants = upstream 6.0.0's text (the strings
+    hec_strerror returns for codes 1..13), and EcShardError's = helyim's
+    thiserror formats (errors.rs:56-65, Underflow's `{0}` twice kept)."""
+    from helyim_amd import _lib
+    src = _wrapper_src()
+    disp = src[src.index("impl fmt::Display for Error {"):]
+    disp = disp[:disp.index("impl std::error::Error for Error")]
+    arms = dict(re.findall(r"\b([A-Z]\w+) => \"([^\"]+)\",", disp))
+    order = _variants(src, "Error")[:13]
+    assert len(arms) == 13
+    for code, name in enumerate(order, start=1):
+        assert arms[name] == _lib.strerror(code), (name, arms[name])
+    ec = src[src.index("impl fmt::Display for EcShardError {"):]
+    ec = _squash(ec[:ec.index("impl std::error::Error for EcShardError")])
+    for want in ('EcShardError::Io(e) => write!(f, "Io error: {e}")',
+                 'EcShardError::ErasureCoding(e) => write!(f, "Erasure coding error: {e}")',
+                 'EcShardError::Underflow(a, _) => write!(f, "Only {a} shards found but {a} required")',
+                 'EcShardError::UnexpectedEcShardSize(a, b) => write!(f, "ec shard size expected {a} but actually is {b}")',
+                 'EcShardError::UnexpectedBlockSize(a, b) => write!(f, "unexpected block size {a}, buffer size {b}")'):
+        assert want in ec, want
+
+
+def test_file_errors_rebuilt_from_last_error_values():
+    """file_err rebuilds the payloads from hec_last_error_values: the io::Error
+    from the errno (what File::open's `?` gives helyim), the two usizes of the
+    size variants; RS and device codes wrap as ErasureCoding (errors.rs:58-59)."""
+    src = _squash(_wrapper_src())
+    body = src[src.index("fn file_err(code: c_int) -> EcShardError {"):]
+    body = body[:body.index("fn cstr(")]
+    assert "let (a, b, errno) = last_error_values();" in body
+    assert "sys::HEC_ERR_IO if errno != 0 => EcShardError::Io(io::Error::from_raw_os_error(errno))" in body
+    for v, c in (("Underflow", "UNDERFLOW"), ("UnexpectedEcShardSize", "UNEXPECTED_EC_SHARD_SIZE"),
+                 ("UnexpectedBlockSize", "UNEXPECTED_BLOCK_SIZE")):
+        assert f"sys::HEC_ERR_{c} => EcShardError::{v}(a as usize, b as usize)" in body, v
+    assert "c => EcShardError::ErasureCoding(to_err(c))" in body
+    assert "unsafe { sys::hec_last_error_values(&mut a, &mut b, &mut e) }" in src

@@ -110,6 +110,7 @@ SIGNATURES = {
     "hec_host_numa_node": (_I, [_P, ctypes.POINTER(_I)]),
     "hec_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hec_decode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
+    "hec_ragged_kernel_name": (ctypes.c_char_p, [_P, _U32, _I]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

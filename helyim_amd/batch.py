@@ -198,6 +198,17 @@ def reconstruct_ragged(rs: ReedSolomon, base: torch.Tensor, descs, bad_stripes: 
                                          _stream_ptr(stream)))
 
 
+def ragged_kernel_name(descs, decode: bool) -> str:
+    """The kernel (and workgroup order) encode_ragged / reconstruct_ragged runs
+    on these descriptors under the current knobs (hec_ragged_kernel_name: the
+    launch's own choice)."""
+    import numpy as np
+    d = descs if isinstance(descs, np.ndarray) and descs.dtype == desc_dtype() else \
+        np.array([tuple(int(x) for x in r) for r in descs], dtype=desc_dtype())
+    d = np.ascontiguousarray(d)
+    return lib.hec_ragged_kernel_name(d.ctypes.data if len(d) else None, len(d), int(bool(decode))).decode()
+
+
 def fill_splitmix(t: torch.Tensor, bytes_per_stripe: int, seed_base: int, stream=None) -> None:
     """Fill the first bytes_per_stripe bytes of each t[s] with splitmix64(seed_base + s)."""
     if t.dtype != torch.uint8 or not t.is_cuda or t.dim() < 1:

@@ -295,6 +295,36 @@ uint64_t ragged_chunks(const hec_stripe_desc& d, bool decode, uint32_t chunk_byt
     return (uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes;
 }
 
+// The kernel and workgroup order of one ragged launch, shared by gpu_ragged
+// and hec_ragged_kernel_name so a reported name is the kernel that runs.
+struct RaggedPick {
+    bool bitslice;  // encode with every length a multiple of 8 KiB: rs104_bs_ragged_kernel
+    bool remap;     // XCD eighths (else dispatch order)
+};
+RaggedPick ragged_pick(const hec_stripe_desc* descs, uint32_t n, bool decode, const LaunchConfig& cfg) {
+    RaggedPick p;
+    p.bitslice = !decode && cfg.bitslice != 0 && cfg.mode == 0;
+    for (uint32_t j = 0; j < n && p.bitslice; ++j) p.bitslice = descs[j].shard_len % kBsChunk == 0;
+    // XCD eighths: the ragged decode +2% on the bench batch (with the no-op
+    // skip +10% on the mixed workload, profiles/r02/ab_ragged_remap_skip.jsonl);
+    // the bit-sliced ragged encode +2% at 512 mixed stripes, +7% at 4096 and
+    // +9% on uniform 4 MiB stripes (profiles/r03/sweep_mixed2.jsonl). The
+    // global knob (hec_set_launch_config xcd_remap 0) turns both off.
+    p.remap = cfg.xcd_remap == 1 && (decode || cfg.ragged_encode_remap != 0);
+    return p;
+}
+
+const char* ragged_name(const RaggedPick& p, bool decode) {
+    if (decode)
+        return p.remap ? "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
+                       : "rs104_ragged_kernel<DEC=true> (table lookup, dispatch order)";
+    if (p.bitslice)
+        return p.remap ? "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
+                       : "rs104_bs_ragged_kernel (bit-sliced, dispatch order)";
+    return p.remap ? "rs104_ragged_kernel<DEC=false> (table lookup, XCD eighths)"
+                   : "rs104_ragged_kernel<DEC=false> (table lookup, dispatch order)";
+}
+
 // Device-resident ragged batches: stripe descriptors come from the host, data
 // stays in HBM. Descriptors -> RaggedItems + workgroup map in pinned staging,
 // uploaded on the caller's stream ahead of the kernel.
@@ -303,10 +333,9 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     if (!rs || !d_base || (n && !descs)) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
     if (!(rs->k == 10 && rs->m == 4))
         return fail(HEC_ERR_INVALID_ARGUMENT, "ragged device batches are RS(10,4) only");
-    // encode of lengths that are all multiples of 8 KiB: the bit-sliced kernel
     const LaunchConfig cfg = launch_config();
-    bool bitslice = !decode && cfg.bitslice != 0 && cfg.mode == 0;
-    for (uint32_t j = 0; j < n && bitslice; ++j) bitslice = descs[j].shard_len % kBsChunk == 0;
+    const RaggedPick pick = ragged_pick(descs, n, decode, cfg);
+    const bool bitslice = pick.bitslice;
     const uint32_t chunk_bytes = bitslice ? kBsChunk : 4096;
     uint64_t n_blocks = 0;
     for (uint32_t j = 0; j < n; ++j) {
@@ -353,11 +382,7 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     ra.tabs = decode ? gd->decode_dense.tabs : gd->encode.tabs;
     ra.lut = decode ? gd->decode_dense.lut : nullptr;
     ra.bad_count = d_bad;
-    // XCD eighths: the ragged decode +2% on the bench batch (with the no-op
-    // skip +10% on the mixed workload, profiles/r02/ab_ragged_remap_skip.jsonl);
-    // the bit-sliced ragged encode +2% at 512 mixed stripes, +7% at 4096 and
-    // +9% on uniform 4 MiB stripes (profiles/r03/sweep_mixed2.jsonl)
-    ra.xcd_remap = (decode ? cfg.xcd_remap == 1 : cfg.ragged_encode_remap != 0) ? 1u : 0u;
+    ra.xcd_remap = pick.remap ? 1u : 0u;
     if (n_blocks == 0) {  // every stripe already complete (upstream no-op)
         HEC_HIP(hipEventRecord(slot.free, stream));
         return HEC_OK;
@@ -383,6 +408,11 @@ int hec_gpu_encode_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_
 int hec_gpu_reconstruct_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs,
                                uint32_t n_stripes, uint32_t* d_bad_stripes, void* stream) {
     return hec::gpu_ragged(rs, d_base, descs, n_stripes, true, d_bad_stripes, static_cast<hipStream_t>(stream));
+}
+
+const char* hec_ragged_kernel_name(const hec_stripe_desc* descs, uint32_t n_stripes, int decode) {
+    if (n_stripes && !descs) return "invalid argument";
+    return hec::ragged_name(hec::ragged_pick(descs, n_stripes, decode != 0, hec::launch_config()), decode != 0);
 }
 
 }  // extern "C"

@@ -427,7 +427,9 @@ int hec_set_encode_kernel(int kind);
 /* Ragged device encodes (hec_gpu_encode_ragged): 1 = the workgroups of one
  * XCD take a contiguous eighth of the launch's column ranges, as the decodes
  * do with xcd_remap 1 (default; 3-9% faster on the mixed workload, DESIGN.md
- * §4), 0 = dispatch order. Speed only. Returns HEC_OK. */
+ * §4), 0 = dispatch order. Applies while the global xcd_remap is 1
+ * (hec_set_launch_config xcd_remap 0 turns every remap off). Speed only.
+ * Returns HEC_OK. */
 int hec_set_ragged_encode_remap(int on);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
@@ -450,6 +452,10 @@ const char* hec_version(void);
 const char* hec_encode_kernel_name(uint64_t shard_len);
 /* Same for a 16-byte-aligned in-place RS(10,4) device batch reconstruct. */
 const char* hec_decode_kernel_name(uint64_t shard_len);
+/* Kernel (and workgroup order) hec_gpu_encode_ragged (decode = 0) or
+ * hec_gpu_reconstruct_ragged (decode != 0) runs on these descriptors under the
+ * current knobs: the same choice the launch makes (static string). */
+const char* hec_ragged_kernel_name(const hec_stripe_desc* descs, uint32_t n_stripes, int decode);
 
 #ifdef __cplusplus
 }

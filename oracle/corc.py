@@ -137,3 +137,82 @@ def read_ec_data(base: str, ranges, large: int = 1 << 30, small: int = 1 << 20, 
     rc = lib().orc_read_ec_data(base.encode(), large, small, offs.ctypes.data, sizes.ctypes.data, n,
                                 out.ctypes.data, int(simd))
     return rc, out[:total].tobytes()
+
+
+GAMMA = 0x9E3779B97F4A7C15
+
+
+def shard_seed(seed: int, shard: int, shard_len: int) -> int:
+    """splitmix64 seed of shard `shard` of a stripe seeded `seed` (its stream
+    from word shard * L / 8 on; L a multiple of 8)."""
+    return (seed + shard * (shard_len // 8) * GAMMA) & ((1 << 64) - 1)
+
+
+def check_stripes(host: np.ndarray, masks=None, threads: int = 16, data_seeds=None) -> List[int]:
+    """Bit-exact check of a chunk of RS(10,4) stripes against the C oracle, on
+    a pool of threads (ctypes releases the GIL inside the C calls).
+
+    host: [S, 14, L] uint8, each shard contiguous.
+    * Always: every stripe's parity (shards 10..13) == the oracle's encode of
+      its data shards 0..9.
+    * data_seeds [S] (stripe s = splitmix64_bytes(data_seeds[s], 10 L)): the
+      data shards also equal that stream, so the whole stripe is the oracle's
+      codeword of the seeded data.
+    * masks [S]: every shard erased in masks[s] (bit clear) also equals the
+      oracle's reconstruct (upstream rule: first 10 present shards) from the
+      present ones (stripes with all 14 or fewer than 10 present: skipped).
+    Returns the indices of the stripes that differ (sorted)."""
+    from concurrent.futures import ThreadPoolExecutor
+    S, n, L = host.shape
+    assert n == 14 and host.dtype == np.uint8
+    rs = CReedSolomon(10, 4)
+    full = (1 << 14) - 1
+    if data_seeds is not None:
+        assert L % 8 == 0, "seeded data check needs L % 8 == 0"
+
+    def shard(s, i):
+        return np.ascontiguousarray(host[s, i])
+
+    def one(s):
+        data = [shard(s, i) for i in range(10)]
+        if data_seeds is not None:
+            for i in range(10):
+                if not np.array_equal(data[i], splitmix64_bytes(shard_seed(int(data_seeds[s]), i, L), L)):
+                    return False
+        par = [np.empty(L, np.uint8) for _ in range(4)]
+        rs.encode(data + par)
+        if not all(np.array_equal(par[j], host[s, 10 + j]) for j in range(4)):
+            return False
+        if masks is None:
+            return True
+        m = int(masks[s]) & full
+        if m == full or bin(m).count("1") < 10:
+            return True
+        present = [bool((m >> i) & 1) for i in range(14)]
+        bufs = [shard(s, i) if present[i] else np.empty(L, np.uint8) for i in range(14)]
+        if rs.reconstruct(bufs, present) != 0:
+            return False
+        return all(np.array_equal(bufs[i], host[s, i]) for i in range(14) if not present[i])
+
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        ok = list(ex.map(one, range(S)))
+    return [s for s in range(S) if not ok[s]]
+
+
+def check_device_batch(t, masks=None, data_seeds=None, chunk: int = 64, threads: int = 16) -> List[int]:
+    """check_stripes over a whole device batch t [S, 14, L] (torch, any shard
+    and stripe strides), copied back `chunk` stripes at a time through one
+    pinned host buffer. Returns the stripe indices that differ."""
+    import torch
+    S, n, L = t.shape
+    c = min(chunk, S)
+    pinned = torch.empty((c, n, L), dtype=torch.uint8, pin_memory=True)
+    bad = []
+    for s0 in range(0, S, c):
+        s1 = min(S, s0 + c)
+        h = pinned[:s1 - s0]
+        h.copy_(t[s0:s1])
+        m = None if masks is None else masks[s0:s1]
+        seeds = None if data_seeds is None else data_seeds[s0:s1]
+        bad += [s0 + s for s in check_stripes(h.numpy(), m, threads, seeds)]
+    return bad

@@ -200,4 +200,5 @@ extern "C" {
     pub fn hec_version() -> *const c_char;
     pub fn hec_encode_kernel_name(shard_len: u64) -> *const c_char;
     pub fn hec_decode_kernel_name(shard_len: u64) -> *const c_char;
+    pub fn hec_ragged_kernel_name(descs: *const hec_stripe_desc, n_stripes: u32, decode: c_int) -> *const c_char;
 }

@@ -300,3 +300,33 @@ def test_kernel_name_follows_dispatch_under_every_knob():
         lib.hec_set_launch_config(1, 0, 1, 0)
         lib.hec_set_decode_vector_bytes(8)
         lib.hec_set_encode_vector_bytes(16)
+
+
+def test_ragged_kernel_name_follows_the_launch_choice():
+    """hec_ragged_kernel_name comes from the ragged launch's own pick
+    (ragged_pick in intervals.cpp): bit-sliced only when every length is a
+    multiple of 8 KiB, XCD eighths unless the ragged-encode knob or the global
+    xcd_remap (the global knob now covers ragged encodes) is off."""
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    lib = H.lib
+    aligned = [(0, 65536, 65536, 0x3FFF), (14 * 65536, 8192, 8192, 0x3FF0)]
+    odd = aligned + [(14 * 65536 + 14 * 8192, 8192, 4096, 0x3FFF)]
+    try:
+        assert B.ragged_kernel_name(aligned, False) == "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
+        assert B.ragged_kernel_name(odd, False) == "rs104_ragged_kernel<DEC=false> (table lookup, XCD eighths)"
+        assert B.ragged_kernel_name(aligned, True) == "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
+        assert lib.hec_set_ragged_encode_remap(0) == 0
+        assert B.ragged_kernel_name(aligned, False).endswith("(bit-sliced, dispatch order)")
+        assert B.ragged_kernel_name(aligned, True).endswith("XCD eighths)")  # decodes follow the global knob
+        assert lib.hec_set_ragged_encode_remap(1) == 0
+        assert lib.hec_set_launch_config(1, 0, 0, 0) == 0
+        assert B.ragged_kernel_name(aligned, False).endswith("(bit-sliced, dispatch order)")
+        assert B.ragged_kernel_name(aligned, True).endswith("(table lookup, dispatch order)")
+        assert lib.hec_set_launch_config(1, 0, 1, 0) == 0
+        assert lib.hec_set_encode_kernel(0) == 0
+        assert B.ragged_kernel_name(aligned, False).startswith("rs104_ragged_kernel<DEC=false>")
+    finally:
+        lib.hec_set_ragged_encode_remap(1)
+        lib.hec_set_launch_config(1, 0, 1, 0)
+        lib.hec_set_encode_kernel(1)

@@ -31,6 +31,8 @@ def test_bench_line_contract():
     assert d["unit"] == "GiB/s" and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["dtype"] == "u8" and d["vs_baseline"] is None
     assert d["verified"] is True
+    v = d["verification"]  # the whole batch against the C oracle, not a sample
+    assert v["stripes_checked"] == S and v["rebuilt_shards_checked"] == 4 * S and v["mismatched_stripes"] == []
     assert d["config"]["stripes_per_gpu"] == S and d["config"]["shard_len"] == L
     # value = encode + decode data payload over the timed steps
     payload = 2 * S * 10 * L
@@ -59,3 +61,28 @@ def test_bench_multi_gpu_host_leg_child():
     d = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
     assert d["devices"] == [0, 0] and d["stripes"] == 512
     assert d["encode_data_GiB_s"] > 1 and d["decode_data_GiB_s"] > 1
+
+
+@pytest.mark.gpu
+def test_bench_mixed_leg_verified_and_named_by_the_launcher(gpu):
+    """The config-5 leg (bench.mixed_section) on 256 stripes: its kernel names
+    are the ragged launch's own choice (hec_ragged_kernel_name), and its
+    oracle check covers every (length, erasure count) pair the batch has."""
+    import bench
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    m = bench.mixed_section(rs, 0, n_stripes=256, e2e_stripes=32)
+    v = m["verification"]
+    assert v["ok"] and v["mismatched_stripes"] == [] and v["stripes_checked"] >= 64
+    assert v["erasure_counts"] == [0, 1, 2, 3, 4] and len(v["shard_lens"]) == 7
+    assert m["encode"]["kernel"] == "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
+    assert m["decode"]["kernel"] == "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
+    try:  # the names follow the knobs, as the launch does
+        H.lib.hec_set_ragged_encode_remap(0)
+        m2 = bench.mixed_section(rs, 1, n_stripes=96, e2e_stripes=8)
+        assert m2["encode"]["kernel"] == "rs104_bs_ragged_kernel (bit-sliced, dispatch order)"
+        assert m2["verification"]["ok"]
+    finally:
+        H.lib.hec_set_ragged_encode_remap(1)
+    assert B.ragged_kernel_name([(0, 4096, 4096, 0)], False).startswith("rs104_ragged_kernel<DEC=false>")

@@ -97,6 +97,7 @@ SIGNATURES = {
     "hec_set_encode_kernel": (_I, [_I]),
     "hec_set_ragged_encode_remap": (_I, [_I]),
     "hec_set_host_zero_copy": (_I, [_I]),
+    "hec_host_staging_stats": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "hec_set_xcd_parts": (_I, [_I]),
     "hec_set_chunk_rotation": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
@@ -106,6 +107,7 @@ SIGNATURES = {
     "hec_device_numa_node": (_I, [_I, ctypes.POINTER(_I)]),
     "hec_bind_thread_to_device": (_I, [_I, ctypes.POINTER(_I)]),
     "hec_host_alloc": (_I, [_S, ctypes.POINTER(_P)]),
+    "hec_host_alloc_multi": (_I, [_P, _S, _U64, _U32, ctypes.POINTER(_P)]),
     "hec_host_free": (_I, [_P]),
     "hec_host_numa_node": (_I, [_P, ctypes.POINTER(_I)]),
     "hec_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),

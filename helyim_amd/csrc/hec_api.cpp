@@ -136,11 +136,40 @@ class HostPool {
 };
 }  // namespace
 
+// Pools per device (up to kPoolsPerDevice each, created on first use and
+// never destroyed: their threads live for the process). A call takes a free
+// pool of its current device, so the ranges of one multi-device host call --
+// and concurrent callers on different GPUs -- copy on their own workers
+// instead of all but one running serially. A pool's threads
+// inherit the CPU affinity of the thread that created it: a range thread
+// bound to its GPU's NUMA node (run_device_ranges) gets workers on that node.
+constexpr size_t kPoolsPerDevice = 2;
 void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>& fn) {
-    // created on first use and never destroyed (threads live for the process)
-    static HostPool* pool = new HostPool(15);
-    if (!pool->run(n, max_threads, fn))
-        for (size_t i = 0; i < n; ++i) fn(i);
+    static std::mutex mu;
+    static auto* pools = new std::map<int, std::vector<HostPool*>>();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = 0;
+    }
+    std::vector<HostPool*> mine;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        mine = (*pools)[dev];
+    }
+    for (HostPool* p : mine)
+        if (p->run(n, max_threads, fn)) return;
+    HostPool* fresh = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto& v = (*pools)[dev];
+        if (v.size() < kPoolsPerDevice) {
+            fresh = new HostPool(15);
+            v.push_back(fresh);
+        }
+    }
+    if (fresh && fresh->run(n, max_threads, fn)) return;
+    for (size_t i = 0; i < n; ++i) fn(i);  // every pool of this device busy: this thread alone
 }
 
 // Process-wide launch knobs (measurement switches, speed only): set under a

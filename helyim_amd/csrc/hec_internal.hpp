@@ -170,6 +170,7 @@ template <typename S>
 struct Lease {
     S* sc = nullptr;
     std::unique_lock<std::mutex> lk;
+    size_t index = 0;  // the slot's creation order in its pool
 };
 // Per-device pool of S (S has `std::mutex mu` and `int init()`, called once
 // when a slot is created).
@@ -181,11 +182,12 @@ struct SlotPool {
     int lease(Lease<S>& out) {
         {
             std::lock_guard<std::mutex> g(mu);
-            for (auto& sl : slots) {
-                std::unique_lock<std::mutex> l(sl->mu, std::try_to_lock);
+            for (size_t i = 0; i < slots.size(); ++i) {
+                std::unique_lock<std::mutex> l(slots[i]->mu, std::try_to_lock);
                 if (l.owns_lock()) {
-                    out.sc = sl.get();
+                    out.sc = slots[i].get();
                     out.lk = std::move(l);
+                    out.index = i;
                     return 0;
                 }
             }
@@ -194,10 +196,12 @@ struct SlotPool {
                 if (int rc = s->init()) return rc;
                 out.lk = std::unique_lock<std::mutex>(s->mu);
                 out.sc = s.get();
+                out.index = slots.size();
                 slots.push_back(std::move(s));
                 return 0;
             }
-            out.sc = slots[rr++ % slots.size()].get();
+            out.index = rr++ % slots.size();
+            out.sc = slots[out.index].get();
         }
         out.lk = std::unique_lock<std::mutex>(out.sc->mu);  // every slot busy: wait for one
         return 0;
@@ -231,11 +235,12 @@ using CompactTake = std::function<void(size_t job, int shard, const uint8_t* src
 int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& jobs, const CompactFill& fill,
                             const CompactTake& take, bool io_bound_fill = false);
 
-// Run fn(i) for i in [0, n) on the library's persistent host worker pool
-// (host memcpy of staging): up to 16 threads, at least 1 MiB of `bytes` per
-// thread and 4 MiB in all (below that, waking workers costs more than the
-// copy saves: measured at 256 KiB shards, tools/bench_latency.py).
-// Concurrent callers do not wait for each other: a call that finds the pool
+// Run fn(i) for i in [0, n) on a persistent host worker pool of the calling
+// thread's current device (host memcpy of staging): up to 16 threads, at
+// least 1 MiB of `bytes` per thread and 4 MiB in all (below that, waking
+// workers costs more than the copy saves: measured at 256 KiB shards,
+// tools/bench_latency.py). Each device has up to 2 pools; concurrent callers
+// do not wait for each other: a call that finds every pool of its device
 // busy runs serially on its own thread.
 void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>& fn);
 

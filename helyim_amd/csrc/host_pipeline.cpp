@@ -42,6 +42,30 @@ struct Pipeline {
         return HEC_OK;
     }
     int init() { return HEC_OK; }  // streams and slots are made on first use (reserve)
+    // Staging bytes held (pinned host, device).
+    uint64_t pinned_bytes() const {
+        return (hslot[0] ? 2 * hslot_cap : 0) + (mask_host[0] ? uint64_t(kDepth) * mask_cap * 4 : 0);
+    }
+    uint64_t device_bytes() const {
+        return (slot[0] ? uint64_t(kDepth) * slot_cap : 0) + (mask_dev[0] ? uint64_t(kDepth) * mask_cap * 4 : 0);
+    }
+    // Free the large staging (the pageable path's pinned slots and the copy
+    // path's device slots); streams, events and mask words stay. The next
+    // call on this pipeline reserves again.
+    void trim() {
+        for (auto& st : streams)  // (calls end synchronised; this is belt and braces)
+            if (st) (void)hipStreamSynchronize(st);
+        for (auto& h : hslot) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+        }
+        hslot_cap = 0;
+        for (auto& d : slot) {
+            if (d) (void)hipFree(d);
+            d = nullptr;
+        }
+        slot_cap = 0;
+    }
     ~Pipeline() {
         for (auto& h : hslot) (void)hipHostFree(h);
         for (auto& e : hdone)
@@ -84,21 +108,45 @@ struct Pipeline {
 
 // Per-device pool of pipelines (SlotPool, hec_internal.hpp): concurrent host
 // batches on one device -- other threads, or two ranges of one multi-device
-// call on the same GPU -- each lease their own streams and slots.
-int lease_pipeline(Lease<Pipeline>& out) {
-    static std::mutex mu;
+// call on the same GPU -- each lease their own streams and slots. Up to
+// kScratchSlots (8) pipelines exist per device, but only the first
+// kWarmPipelines keep their staging between calls: a pipeline created by a
+// burst of concurrent calls frees its large buffers when its call ends
+// (PipelineLease), so the steady footprint per device is that of two
+// pipelines (INTEGRATION.md §5 states the worst case).
+constexpr size_t kWarmPipelines = 2;
+std::mutex& pipeline_reg_mu() {
+    static std::mutex* m = new std::mutex();
+    return *m;
+}
+std::map<int, std::unique_ptr<SlotPool<Pipeline>>>& pipeline_reg() {
     static auto* reg = new std::map<int, std::unique_ptr<SlotPool<Pipeline>>>();  // process lifetime
+    return *reg;
+}
+
+struct PipelineLease {
+    Lease<Pipeline> lease;
+    bool trim_after = false;
+    Pipeline* operator->() const { return lease.sc; }
+    ~PipelineLease() {
+        if (trim_after && lease.sc) lease.sc->trim();  // still holding the pipeline's mutex
+    }
+};
+
+int lease_pipeline(PipelineLease& out) {
     int dev;
     int rc = current_device(&dev);
     if (rc) return rc;
     SlotPool<Pipeline>* pool;
     {
-        std::lock_guard<std::mutex> lk(mu);
-        auto& p = (*reg)[dev];
+        std::lock_guard<std::mutex> lk(pipeline_reg_mu());
+        auto& p = pipeline_reg()[dev];
         if (!p) p.reset(new SlotPool<Pipeline>());
         pool = p.get();
     }
-    return pool->lease(out);
+    if ((rc = pool->lease(out.lease))) return rc;
+    out.trim_after = out.lease.index >= kWarmPipelines;
+    return HEC_OK;
 }
 
 // Copy `rows` rows of `width` bytes with pitches (2D; 1D when both are dense).
@@ -169,10 +217,8 @@ int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
             return fail(HEC_ERR_INVALID_ARGUMENT,
                         "device " + std::to_string(devices[r]) + " of " + std::to_string(count) + " in the list");
     if (n_stripes == 0) return HEC_OK;
-    // The process-wide host worker pool starts on its first use and its
-    // threads inherit that thread's CPU affinity: start it here, from the
-    // caller's thread, not from a range thread bound to one GPU's node.
-    pool_run(0, 1, [](size_t) {});
+    // (Each device's host worker pools start on first use from a range thread
+    // already bound to that GPU's node, so their workers copy on that node.)
     const size_t R = std::min<size_t>(n_devices, n_stripes);
     std::vector<int> rcs(R, HEC_OK);
     std::vector<std::string> details(R);
@@ -236,9 +282,9 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
         return rc;
     GeomDevice* gd;
     if ((rc = geom_device(rs, &gd))) return rc;
-    Lease<Pipeline> lease;
+    PipelineLease lease;
     if ((rc = lease_pipeline(lease))) return rc;
-    Pipeline* p = lease.sc;
+    Pipeline* p = lease.lease.sc;
     const int k = rs->k, m = rs->m;
     uint8_t *zd, *zp;
     if (host_device_view(h_data, batch_span(data_stripe_stride, data_shard_stride, k, shard_len, n_stripes), &zd) &&
@@ -330,9 +376,9 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
     if ((rc = check_strided("shards", uint32_t(rs->n), stripe_stride, shard_stride, shard_len, n_stripes))) return rc;
     GeomDevice* gd;
     if ((rc = geom_device(rs, &gd))) return rc;
-    Lease<Pipeline> lease;
+    PipelineLease lease;
     if ((rc = lease_pipeline(lease))) return rc;
-    Pipeline* p = lease.sc;
+    Pipeline* p = lease.lease.sc;
     const int k = rs->k, n = rs->n;
     const uint32_t full = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
     uint8_t* zs;
@@ -514,6 +560,33 @@ int hec_host_reconstruct_batch_multi(const hec_rs_t* rs, const int* devices, siz
     if (rc) return rc;
     if (n_bad_stripes)
         for (uint32_t b : bad) *n_bad_stripes += b;
+    return HEC_OK;
+}
+
+int hec_host_staging_stats(int* n_pipelines, uint64_t* pinned_bytes, uint64_t* device_bytes) {
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    SlotPool<Pipeline>* pool = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(pipeline_reg_mu());
+        auto it = pipeline_reg().find(dev);
+        if (it != pipeline_reg().end()) pool = it->second.get();
+    }
+    int n = 0;
+    uint64_t pinned = 0, devb = 0;
+    if (pool) {
+        std::lock_guard<std::mutex> g(pool->mu);
+        for (auto& sl : pool->slots) {
+            std::lock_guard<std::mutex> l(sl->mu);  // waits for a call in flight on it
+            ++n;
+            pinned += sl->pinned_bytes();
+            devb += sl->device_bytes();
+        }
+    }
+    if (n_pipelines) *n_pipelines = n;
+    if (pinned_bytes) *pinned_bytes = pinned;
+    if (device_bytes) *device_bytes = devb;
     return HEC_OK;
 }
 

@@ -6,11 +6,14 @@
 // CPUs to that node too.
 //
 // Node of a GPU: sysfs numa_node of its PCI function (hipDeviceGetPCIBusId).
-// Placement: the allocating thread's memory policy is set to MPOL_BIND on that
-// node around hipHostMalloc(hipHostMallocNumaUser), which makes the runtime
-// follow the thread's policy when it backs the pinned range, then restored.
+// Placement: the allocating thread's memory policy is set to MPOL_PREFERRED on
+// that node around hipHostMalloc(hipHostMallocNumaUser), which makes the
+// runtime follow the thread's policy when it backs the pinned range, then
+// restored. One host batch split over several GPUs (hec_host_alloc_multi) gets
+// each stripe range's pages on its own GPU's node (mbind).
 // Raw syscalls, so libhec needs no libnuma.
 #include <sched.h>
+#include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -19,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -28,8 +32,9 @@ namespace hec {
 namespace {
 
 constexpr int kMpolDefault = 0;
-constexpr int kMpolBind = 2;
+constexpr int kMpolPreferred = 1;
 constexpr unsigned kMaxNodes = 1024;
+constexpr size_t kMaskWords = kMaxNodes / (8 * sizeof(unsigned long));
 
 std::string read_line(const std::string& path) {
     std::ifstream f(path);
@@ -86,9 +91,9 @@ int device_numa_node(int device, int* node) {
     return HEC_OK;
 }
 
-// Test hook: HEC_TEST_NUMA_BIND_FAIL=1 makes every NUMA-bound allocation
-// attempt fail as if the node were full, so the fallback below runs on any
-// machine (tests/test_gpu_numa.py).
+// Test hook: HEC_TEST_NUMA_BIND_FAIL=1 makes every NUMA-placed allocation
+// attempt fail after it ran, as if the node could not back it, so the
+// fallback below runs on any machine (tests/test_gpu_numa.py).
 static bool bind_failure_forced() {
     static const bool forced = [] {
         const char* v = std::getenv("HEC_TEST_NUMA_BIND_FAIL");
@@ -98,42 +103,76 @@ static bool bind_failure_forced() {
 }
 
 // Pinned host memory on the current device's NUMA node (plain hipHostMalloc
-// when the node is unknown or the machine has one node). Placement is a speed
-// preference, never a requirement: when the node cannot back the range
-// (MPOL_BIND and its free memory is short), the allocation is retried under
-// the default policy (any node) instead of failing.
+// when the node is unknown or the machine has one node). The allocating
+// thread's policy is MPOL_PREFERRED on the node around
+// hipHostMalloc(hipHostMallocNumaUser): placement is a speed preference,
+// never a requirement, so a short node spills to the others page by page
+// (MPOL_BIND would wake the constrained OOM killer during pinning instead of
+// failing). Should the placed attempt still fail, the allocation is retried
+// under the default policy instead of failing.
 int pinned_alloc(void** p, size_t bytes) {
     *p = nullptr;
     int dev, node = -1, rc;
     if ((rc = current_device(&dev))) return rc;
     if ((rc = device_numa_node(dev, &node))) return rc;
-    const bool forced = bind_failure_forced();
-    if (!forced && (node < 0 || node >= int(kMaxNodes) || online_nodes() < 2)) {
-        HEC_HIP(hipHostMalloc(p, bytes, hipHostMallocDefault));
+    const unsigned flags = hipHostMallocPortable;  // every device may code it zero-copy (_multi ranges)
+    if (node < 0 || node >= int(kMaxNodes) || online_nodes() < 2) {
+        HEC_HIP(hipHostMalloc(p, bytes, flags));
         return HEC_OK;
     }
-    if (forced) {
-        HEC_HIP(hipHostMalloc(p, bytes, hipHostMallocDefault));  // the fallback's allocation
-        return HEC_OK;
-    }
-    unsigned long old_mask[kMaxNodes / (8 * sizeof(unsigned long))] = {0};
+    unsigned long old_mask[kMaskWords] = {0};
     int old_mode = kMpolDefault;
     const bool saved = syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNodes, nullptr, 0) == 0;
-    unsigned long mask[kMaxNodes / (8 * sizeof(unsigned long))] = {0};
+    unsigned long mask[kMaskWords] = {0};
     mask[node / (8 * sizeof(unsigned long))] = 1ul << (node % (8 * sizeof(unsigned long)));
-    const bool bound = syscall(SYS_set_mempolicy, kMpolBind, mask, kMaxNodes) == 0;
-    hipError_t e = hipHostMalloc(p, bytes, bound ? hipHostMallocNumaUser : hipHostMallocDefault);
-    if (bound) {
+    const bool placed = syscall(SYS_set_mempolicy, kMpolPreferred, mask, kMaxNodes) == 0;
+    hipError_t e = hipHostMalloc(p, bytes, placed ? (flags | hipHostMallocNumaUser) : flags);
+    if (placed) {
         if (saved) (void)syscall(SYS_set_mempolicy, old_mode, old_mode == kMpolDefault ? nullptr : old_mask,
                                  kMaxNodes);
         else (void)syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0);
     }
+    if (e == hipSuccess && bind_failure_forced()) {  // test hook: as if the placed attempt failed
+        (void)hipHostFree(*p);
+        e = hipErrorOutOfMemory;
+    }
     if (e == hipSuccess) return HEC_OK;
     (void)hipGetLastError();
     *p = nullptr;
-    e = hipHostMalloc(p, bytes, hipHostMallocDefault);  // any node: placement is speed only
+    e = hipHostMalloc(p, bytes, flags);  // any node: placement is speed only
     if (e != hipSuccess) return hip_fail(e, "hipHostMalloc (pinned, after the NUMA-local attempt failed)");
     return HEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Host batches placed per stripe range (hec_host_alloc_multi): anonymous
+// memory, each range's pages preferred on its device's node (mbind before the
+// first touch), then pinned and mapped for every device (hipHostRegister).
+// hec_host_free recognises these by address.
+// ---------------------------------------------------------------------------
+std::mutex& placed_mu() {
+    static std::mutex* m = new std::mutex();
+    return *m;
+}
+std::map<void*, size_t>& placed_allocs() {
+    static auto* m = new std::map<void*, size_t>();  // process lifetime
+    return *m;
+}
+
+// Test hook: HEC_TEST_RANGE_NODES="a,b,..." gives range r node r-th entry
+// instead of its device's node (a one-GPU box lists one device twice).
+std::vector<int> forced_range_nodes() {
+    std::vector<int> v;
+    const char* e = std::getenv("HEC_TEST_RANGE_NODES");
+    if (!e) return v;
+    for (const char* c = e; *c;) {
+        char* end;
+        const long n = std::strtol(c, &end, 10);
+        if (end == c) break;
+        v.push_back(int(n));
+        c = *end == ',' ? end + 1 : end;
+    }
+    return v;
 }
 
 }  // namespace hec
@@ -186,8 +225,82 @@ int hec_host_alloc(size_t bytes, void** out) {
     return pinned_alloc(out, bytes);
 }
 
+int hec_host_alloc_multi(const int* devices, size_t n_devices, uint64_t stripe_stride, uint32_t n_stripes,
+                         void** out) {
+    if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    if (!devices || n_devices == 0 || n_devices > 256)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "device list must have 1..256 entries");
+    uint64_t bytes;
+    if (stripe_stride == 0 || n_stripes == 0 || __builtin_mul_overflow(stripe_stride, uint64_t(n_stripes), &bytes))
+        return fail(HEC_ERR_INVALID_ARGUMENT, "empty or overflowing batch");
+    int count = 0;
+    HEC_TRY(hec_device_count(&count));
+    for (size_t r = 0; r < n_devices; ++r)
+        if (devices[r] < 0 || devices[r] >= count)
+            return fail(HEC_ERR_INVALID_ARGUMENT, "device " + std::to_string(devices[r]) + " out of range");
+    const uint64_t page = uint64_t(sysconf(_SC_PAGESIZE));
+    const uint64_t len = (bytes + page - 1) / page * page;
+    void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return fail_errno(HEC_ERR_OUT_OF_MEMORY, "mmap", errno);
+    // range r = stripes [S*r/R, S*(r+1)/R) -- the split hec_host_*_batch_multi
+    // uses; a page that straddles two ranges goes with the earlier one
+    const size_t R = std::min<size_t>(n_devices, n_stripes);
+    const std::vector<int> forced = forced_range_nodes();
+    const bool multi_node = online_nodes() >= 2;
+    std::vector<std::pair<uint64_t, uint64_t>> spans(R);
+    for (size_t r = 0; r < R; ++r) {
+        const uint64_t s0 = uint64_t(n_stripes) * r / R, s1 = uint64_t(n_stripes) * (r + 1) / R;
+        const uint64_t b0 = r == 0 ? 0 : std::min(len, (s0 * stripe_stride + page - 1) / page * page);
+        const uint64_t b1 = r + 1 == R ? len : std::min(len, (s1 * stripe_stride + page - 1) / page * page);
+        spans[r] = {b0, b1};
+        int node = -1;
+        if (r < forced.size()) node = forced[r];
+        else (void)device_numa_node(devices[r], &node);
+        if (!multi_node || node < 0 || node >= int(kMaxNodes) || b1 <= b0) continue;
+        unsigned long mask[kMaskWords] = {0};
+        mask[node / (8 * sizeof(unsigned long))] = 1ul << (node % (8 * sizeof(unsigned long)));
+        // preferred, not bound: placement is speed only (a short node spills)
+        (void)syscall(SYS_mbind, static_cast<uint8_t*>(p) + b0, b1 - b0, kMpolPreferred, mask, kMaxNodes, 0u);
+    }
+    // first touch under each range's policy, in parallel (the pool's threads
+    // write; the policy belongs to the pages, not to the thread)
+    constexpr uint64_t kTouch = 64ull << 20;
+    const size_t pieces = size_t((len + kTouch - 1) / kTouch);
+    parallel_for(pieces, len, [&](size_t i) {
+        const uint64_t o = i * kTouch;
+        std::memset(static_cast<uint8_t*>(p) + o, 0, size_t(std::min(kTouch, len - o)));
+    });
+    const hipError_t e = hipHostRegister(p, len, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        munmap(p, len);
+        return hip_fail(e, "hipHostRegister");
+    }
+    {
+        std::lock_guard<std::mutex> lk(placed_mu());
+        placed_allocs()[p] = size_t(len);
+    }
+    *out = p;
+    return HEC_OK;
+}
+
 int hec_host_free(void* p) {
     if (!p) return HEC_OK;
+    size_t len = 0;
+    {
+        std::lock_guard<std::mutex> lk(placed_mu());
+        auto it = placed_allocs().find(p);
+        if (it != placed_allocs().end()) {
+            len = it->second;
+            placed_allocs().erase(it);
+        }
+    }
+    if (len) {  // a hec_host_alloc_multi batch
+        const hipError_t e = hipHostUnregister(p);
+        munmap(p, len);
+        if (e != hipSuccess) return hip_fail(e, "hipHostUnregister");
+        return HEC_OK;
+    }
     HEC_HIP(hipHostFree(p));
     return HEC_OK;
 }

@@ -63,6 +63,26 @@ class HostBuffer:
         self._ptr = p.value
         self.nbytes = nbytes
 
+    @classmethod
+    def for_devices(cls, devices, stripe_stride: int, n_stripes: int) -> "HostBuffer":
+        """One host batch of n_stripes stripes for ``host_*_batch(...,
+        devices=devices)`` (hec_host_alloc_multi): each device's stripe range
+        has its pages on that device's NUMA node."""
+        self = cls.__new__(cls)
+        self._ptr = None
+        arr = (ctypes.c_int * len(devices))(*devices)
+        p = ctypes.c_void_p()
+        check(lib.hec_host_alloc_multi(arr, len(devices), stripe_stride, n_stripes, ctypes.byref(p)))
+        self._ptr = p.value
+        self.nbytes = stripe_stride * n_stripes
+        return self
+
+    def numa_node_at(self, offset: int) -> int:
+        """Node holding the page at byte ``offset``."""
+        n = ctypes.c_int(-1)
+        check(lib.hec_host_numa_node(self._ptr + offset, ctypes.byref(n)))
+        return n.value
+
     @property
     def array(self):
         """A fresh numpy view. The view holds this object (through the ctypes
@@ -97,6 +117,7 @@ class HostBuffer:
 
     def __del__(self):
         try:
-            self.close()
+            if getattr(self, "_ptr", None):
+                self.close()
         except Exception:
             pass

@@ -107,6 +107,18 @@ int hec_bind_thread_to_device(int device, int* n_cpus);
 /* Pinned host memory on the current device's NUMA node, addressable by the
  * GPU (host-batch entry points code it zero-copy). Free with hec_host_free. */
 int hec_host_alloc(size_t bytes, void** out);
+/* One pinned host batch of n_stripes * stripe_stride bytes for the _multi
+ * calls over the same device list: range r = stripes [S*r/R, S*(r+1)/R)
+ * (R = min(n_devices, n_stripes), the split hec_host_*_batch_multi uses) has
+ * its pages preferred on devices[r]'s NUMA node (mbind before the first
+ * touch; a page straddling two ranges goes with the earlier one), so on a
+ * two-socket node every GPU's range is read and written on its own socket.
+ * Zero-filled, pinned and mapped for every device (zero-copy for any range).
+ * Placement is speed only: a node short of memory spills to the others.
+ * Free with hec_host_free. Errors: HEC_ERR_INVALID_ARGUMENT (empty list, > 256
+ * entries, a device out of range, empty or overflowing batch). */
+int hec_host_alloc_multi(const int* devices, size_t n_devices, uint64_t stripe_stride, uint32_t n_stripes,
+                         void** out);
 int hec_host_free(void* p);
 /* NUMA node holding the page at p (diagnostic; HEC_ERR_IO if not resident). */
 int hec_host_numa_node(const void* p, int* node);
@@ -439,6 +451,11 @@ int hec_set_host_staging(uint64_t max_bytes);
 /* Host batches on pinned memory: 1 = zero-copy kernels (default), 0 = the
  * copy pipeline. Speed only; identical results. Returns HEC_OK. */
 int hec_set_host_zero_copy(int on);
+/* Diagnostic: host-batch pipelines of the current device (at most 8; only
+ * the first 2 keep their staging between calls, the others free it when
+ * their call ends) and the pinned host / device staging bytes they hold now.
+ * Waits for calls in flight on those pipelines. */
+int hec_host_staging_stats(int* n_pipelines, uint64_t* pinned_bytes, uint64_t* device_bytes);
 /* Host-memory calls coded zero-copy whose input is at most max_bytes learn
  * that the kernel finished from a flag the kernel's last workgroup stores in
  * pinned memory (the caller spins on it, up to 200 us, then falls back to a

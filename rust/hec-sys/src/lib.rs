@@ -85,6 +85,8 @@ extern "C" {
     pub fn hec_device_numa_node(device: c_int, node: *mut c_int) -> c_int;
     pub fn hec_bind_thread_to_device(device: c_int, n_cpus: *mut c_int) -> c_int;
     pub fn hec_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
+    pub fn hec_host_alloc_multi(devices: *const c_int, n_devices: usize, stripe_stride: u64, n_stripes: u32,
+                                out: *mut *mut c_void) -> c_int;
     pub fn hec_host_free(p: *mut c_void) -> c_int;
     pub fn hec_host_numa_node(p: *const c_void, node: *mut c_int) -> c_int;
 
@@ -197,6 +199,7 @@ extern "C" {
     pub fn hec_set_host_staging(max_bytes: u64) -> c_int;
     pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;
     pub fn hec_set_host_zero_copy(on: c_int) -> c_int;
+    pub fn hec_host_staging_stats(n_pipelines: *mut c_int, pinned_bytes: *mut u64, device_bytes: *mut u64) -> c_int;
     pub fn hec_version() -> *const c_char;
     pub fn hec_encode_kernel_name(shard_len: u64) -> *const c_char;
     pub fn hec_decode_kernel_name(shard_len: u64) -> *const c_char;

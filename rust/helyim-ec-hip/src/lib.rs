@@ -451,6 +451,53 @@ pub fn rebuild_ec_files(base_filename: &str) -> Result<Vec<u32>, EcShardError> {
     }
 }
 
+/// Pinned host memory for the host-batch calls, freed on drop
+/// (`hec_host_alloc` / `hec_host_alloc_multi` + `hec_host_free`). Pinned
+/// batches are coded zero-copy.
+pub struct PinnedBuffer {
+    ptr: *mut u8,
+    len: usize,
+}
+unsafe impl Send for PinnedBuffer {}
+unsafe impl Sync for PinnedBuffer {}
+
+impl PinnedBuffer {
+    /// `bytes` on the current device's NUMA node.
+    pub fn new(bytes: usize) -> Result<Self, Error> {
+        let mut p = std::ptr::null_mut();
+        check(unsafe { sys::hec_host_alloc(bytes, &mut p) })?;
+        Ok(Self { ptr: p as *mut u8, len: bytes })
+    }
+
+    /// One packed `[S][total][L]` batch for `encode_batch_multi` /
+    /// `reconstruct_batch_multi` over `devices`: each device's stripe range
+    /// has its pages on that device's NUMA node (`hec_host_alloc_multi`).
+    pub fn for_devices(devices: &[i32], stripe_stride: u64, n_stripes: u32) -> Result<Self, Error> {
+        let mut p = std::ptr::null_mut();
+        check(unsafe { sys::hec_host_alloc_multi(devices.as_ptr(), devices.len(), stripe_stride, n_stripes, &mut p) })?;
+        Ok(Self { ptr: p as *mut u8, len: (stripe_stride * n_stripes as u64) as usize })
+    }
+}
+
+impl std::ops::Deref for PinnedBuffer {
+    type Target = [u8];
+    fn deref(&self) -> &[u8] {
+        unsafe { std::slice::from_raw_parts(self.ptr, self.len) }
+    }
+}
+
+impl std::ops::DerefMut for PinnedBuffer {
+    fn deref_mut(&mut self) -> &mut [u8] {
+        unsafe { std::slice::from_raw_parts_mut(self.ptr, self.len) }
+    }
+}
+
+impl Drop for PinnedBuffer {
+    fn drop(&mut self) {
+        unsafe { sys::hec_host_free(self.ptr as *mut std::os::raw::c_void) };
+    }
+}
+
 /// Multi-GPU servers: whole volumes per GPU, chosen on the
 /// calling thread before the file-layer call.
 pub fn select_device_for_volume(volume_id: u32) -> Result<i32, Error> {

@@ -330,3 +330,19 @@ def test_ragged_kernel_name_follows_the_launch_choice():
         lib.hec_set_ragged_encode_remap(1)
         lib.hec_set_launch_config(1, 0, 1, 0)
         lib.hec_set_encode_kernel(1)
+
+
+def test_host_alloc_multi_arguments_checked_before_device():
+    import helyim_amd as H
+    lib = H.lib
+    p = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert lib.hec_host_alloc_multi(devs, 2, 4096, 4, None) == 66
+    assert lib.hec_host_alloc_multi(None, 0, 4096, 4, ctypes.byref(p)) == 66
+    assert lib.hec_host_alloc_multi(devs, 0, 4096, 4, ctypes.byref(p)) == 66
+    assert lib.hec_host_alloc_multi(devs, 2, 0, 4, ctypes.byref(p)) == 66
+    assert lib.hec_host_alloc_multi(devs, 2, 4096, 0, ctypes.byref(p)) == 66
+    assert lib.hec_host_alloc_multi(devs, 2, 1 << 63, 4, ctypes.byref(p)) == 66  # overflows
+    many = (ctypes.c_int * 257)()
+    assert lib.hec_host_alloc_multi(many, 257, 4096, 4, ctypes.byref(p)) == 66
+    assert p.value is None

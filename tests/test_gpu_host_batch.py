@@ -210,3 +210,116 @@ def test_host_batch_multi_device_generic_geometry(gpu, k, m):
             a[s, int(i)] = 0x3C
     assert B.host_reconstruct_batch(rs, t, masks, devices=[0, 0]) == 0
     assert np.array_equal(a, want)
+
+
+def _multi_roundtrip(t, devices):
+    """encode + 0..4-erasure reconstruct of the host batch t over `devices`,
+    byte-compared with the C oracle."""
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S = t.shape[0]
+    B.host_encode_batch(rs, t, devices=devices)
+    a = t.numpy()
+    want = a.copy()
+    want[:, 10:] = corc.encode_stripes(np.ascontiguousarray(a[:, :10]))
+    assert np.array_equal(a, want)
+    rng = np.random.default_rng(S + 17 * len(devices))
+    masks = np.full(S, (1 << 14) - 1, np.uint32)
+    for s in range(S):
+        for i in rng.choice(14, s % 5, replace=False):
+            masks[s] &= ~np.uint32(1 << int(i))
+            a[s, int(i)] = 0x5A
+    assert B.host_reconstruct_batch(rs, t, masks, devices=devices) == 0
+    assert np.array_equal(a, want)
+
+
+@pytest.mark.parametrize("memory", ["hec_host_alloc", "placed", "torch_pinned", "pageable"])
+def test_host_batch_multi_distinct_devices(gpu, memory):
+    """one host batch over DISTINCT GPUs (each range on its own
+    device; pinned memory allocated under device 0 coded zero-copy by the
+    others, a per-range placed batch, pageable memory) vs the oracle. Needs
+    two or more GPUs: skipped on the one-GPU pool, so distinct-device
+    operation stays unverified there."""
+    import torch
+    import helyim_amd as H
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs >= 2 GPUs (the pool's boxes have one)")
+    devices = list(range(min(n, 8)))
+    S, L = 4 * len(devices) + 3, 65536
+    torch.cuda.set_device(0)
+    buf = None
+    if memory == "hec_host_alloc":
+        buf = H.HostBuffer(S * 14 * L)
+    elif memory == "placed":
+        buf = H.HostBuffer.for_devices(devices, 14 * L, S)
+    if buf is not None:
+        t = buf.tensor((S, 14, L))
+        t.copy_(_host_stripes(S, L, pin=False))
+    else:
+        t = _host_stripes(S, L, pin=memory == "torch_pinned")
+    _multi_roundtrip(t, devices)
+    del t
+    if buf is not None:
+        buf.close()
+
+
+def test_host_batch_multi_on_a_placed_buffer(gpu):
+    """hec_host_alloc_multi's batch (pinned by hipHostRegister, not
+    hipHostMalloc) through the _multi calls over a repeated device list, on
+    both host paths, vs the oracle."""
+    import helyim_amd as H
+    S, L = 9, 65536 + 16
+    buf = H.HostBuffer.for_devices([0, 0, 0], 14 * L, S)
+    t = buf.tensor((S, 14, L))
+    assert int(t.sum()) == 0  # zero-filled
+    t.copy_(_host_stripes(S, L, pin=False))
+    _multi_roundtrip(t, [0, 0, 0])
+    del t
+    buf.close()
+
+
+def test_host_pipeline_pool_trims_after_a_burst(gpu, host_path):
+    """a burst of concurrent host batches may create up to
+    8 pipelines per device, but only the first 2 keep their staging after
+    their call; the pinned and device staging left behind is bounded by two
+    pipelines' worth (hec_host_staging_stats), and every result is exact."""
+    import ctypes
+    import threading
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rs = H.ReedSolomon(10, 4)
+    S, L = 16, 1 << 20
+    src = _host_stripes(S, L, pin=False)
+    want = src.numpy().copy()
+    want[:, 10:] = corc.encode_stripes(np.ascontiguousarray(want[:, :10]))
+    errors, start = [], threading.Barrier(12)
+
+    def work():
+        try:
+            t = src.clone()  # pageable: the staging path
+            start.wait()
+            for _ in range(2):
+                B.host_encode_batch(rs, t)
+            assert np.array_equal(t.numpy(), want)
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append(repr(ex))
+
+    ths = [threading.Thread(target=work) for _ in range(12)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    n, pinned, dev = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+    assert H.lib.hec_host_staging_stats(ctypes.byref(n), ctypes.byref(pinned), ctypes.byref(dev)) == 0
+    Lp = (L + 255) // 256 * 256
+    C = max(1, (96 << 20) // (14 * Lp))
+    per_pinned = 2 * C * 14 * Lp + (1 << 20)  # two pageable-path slots + mask words
+    per_dev = 3 * C * 14 * Lp + (1 << 20)     # three copy-path slots + mask words
+    assert 1 <= n.value <= 8
+    assert pinned.value <= 2 * per_pinned, (n.value, pinned.value)
+    assert dev.value <= 2 * per_dev, (n.value, dev.value)
+    torch.cuda.synchronize()

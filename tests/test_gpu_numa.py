@@ -136,3 +136,66 @@ def test_host_buffer_views_keep_the_buffer_alive():
     del t
     gc.collect()
     assert ref() is None       # freed once the last view is gone
+
+
+def _allowed_nodes():
+    """NUMA nodes this process may allocate on (cgroup cpuset, else online)."""
+    for path in ("/sys/fs/cgroup/cpuset.mems.effective", "/sys/devices/system/node/online"):
+        try:
+            s = open(path).read().strip()
+        except OSError:
+            continue
+        if not s:
+            continue
+        out = []
+        for part in s.split(","):
+            a, _, b = part.partition("-")
+            out += list(range(int(a), int(b) + 1)) if b else [int(a)]
+        return out
+    return [0]
+
+
+def test_multi_device_batch_pages_follow_their_ranges(monkeypatch):
+    """VERDICT r03 "next" 4: hec_host_alloc_multi places each _multi stripe
+    range's pages on its device's node. The one-GPU box lists device 0
+    twice, so a forced node map (HEC_TEST_RANGE_NODES, numa.cpp) stands in for
+    two GPUs on two sockets: placement is read back page by page
+    (move_pages(.., NULL, status) through hec_host_numa_node), then the batch
+    goes through the _multi calls against the C oracle."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    from oracle import corc
+    from oracle import rs_oracle as O
+    nodes = _allowed_nodes()
+    if len(nodes) < 2:
+        pytest.skip(f"one NUMA node allowed here ({nodes})")
+    a, b = nodes[0], nodes[-1]
+    monkeypatch.setenv("HEC_TEST_RANGE_NODES", f"{a},{b}")
+    torch.cuda.set_device(0)
+    S, L = 10, 1 << 20
+    stride = 14 * L
+    buf = H.HostBuffer.for_devices([0, 0], stride, S)
+    page = os.sysconf("SC_PAGE_SIZE")
+    for r, node in ((0, a), (1, b)):
+        s0, s1 = S * r // 2, S * (r + 1) // 2
+        for off in (s0 * stride, (s0 + s1) // 2 * stride + 12345, s1 * stride - page):
+            assert buf.numa_node_at(off) == node, (r, off, buf.numa_node_at(off), node)
+    t = buf.tensor((S, 14, L))
+    for s in range(S):
+        t[s, :10] = torch.from_numpy(corc.splitmix64_bytes(O.STRIPE_SEED_BASE + s, 10 * L).reshape(10, L))
+    rs = H.ReedSolomon(10, 4)
+    B.host_encode_batch(rs, t, devices=[0, 0])
+    want = t.numpy().copy()
+    assert np.array_equal(want[:, 10:], corc.encode_stripes(np.ascontiguousarray(want[:, :10])))
+    masks = np.full(S, (1 << 14) - 1, np.uint32)
+    for s in range(S):
+        for i in ((s, 13, 5 + s % 3, 10)[: s % 5]):
+            masks[s] &= ~np.uint32(1 << int(i))
+            t[s, int(i)] = 0
+    assert B.host_reconstruct_batch(rs, t, masks, devices=[0, 0]) == 0
+    assert np.array_equal(t.numpy(), want)
+    # placement survived the calls (pinned pages do not migrate)
+    assert buf.numa_node_at(0) == a and buf.numa_node_at(S * stride - 1) == b
+    del t
+    buf.close()

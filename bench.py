@@ -484,18 +484,45 @@ def mixed_verify(rs, dev, darr, descs, Ls, es, rank: int) -> dict:
                       "(seeded data, encode, reconstruct from survivors)"}
 
 
-def multi_gpu_e2e_child(ndev: int, timeout_s: float = 240.0) -> dict:
+def multi_gpu_e2e_child(ndev: int, timeout_s: float = 240.0, cmd=None) -> dict:
     """Run e2e_section over devices 0..ndev-1 in a child process (this
-    script with --e2e-multi-child) and return its JSON, or the failure."""
-    cmd = [sys.executable, os.path.abspath(__file__), "--e2e-multi-child", ",".join(str(d) for d in range(ndev))]
+    script with --e2e-multi-child) and return its JSON, or a record of the
+    failure (time limit, exit status, unparsable output): never an exception,
+    so this leg cannot cost the headline line. cmd: override (tests)."""
+    if cmd is None:
+        cmd = [sys.executable, os.path.abspath(__file__), "--e2e-multi-child",
+               ",".join(str(d) for d in range(ndev))]
     try:
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, cwd=ROOT)
     except subprocess.TimeoutExpired:
         return {"error": f"timed out after {timeout_s:.0f} s"}
+    except OSError as ex:
+        return {"error": f"could not start: {ex}"}
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     if p.returncode != 0 or not lines:
         return {"error": f"exit {p.returncode}", "stderr_tail": p.stderr[-800:]}
-    return json.loads(lines[-1])
+    try:
+        return json.loads(lines[-1])
+    except ValueError as ex:
+        return {"error": f"unparsable output: {ex}", "stdout_tail": lines[-1][-400:]}
+
+
+def assemble_host_legs(e2e_all: list, mixed_all: list, world: int) -> dict:
+    """The bench line's end_to_end / mixed sections from every rank's records
+    (gathered on rank 0): one rank's record as is, or per-rank records plus
+    the node aggregate over one wall-clock window."""
+    extras = {"end_to_end": e2e_all[0] if world == 1 else {
+        "aggregate": aggregate_host_path([r["raw"] for r in e2e_all]), "per_rank": e2e_all}}
+    if world == 1:
+        extras["mixed"] = mixed_all[0]
+    else:
+        extras["mixed"] = {"per_rank": mixed_all,
+                           # one wall-clock window over every rank's end-to-end part
+                           "aggregate_end_to_end_data_GiB_s": round(
+                               sum(m["raw"]["payload_bytes"] for m in mixed_all)
+                               / (max(m["raw"]["e2e"][1] for m in mixed_all)
+                                  - min(m["raw"]["e2e"][0] for m in mixed_all)) / 2**30, 2)}
+    return extras
 
 
 def e2e_multi_child_main(devices: list) -> int:
@@ -577,6 +604,8 @@ def parse_args(argv=None):
                     help="GPU-free control-plane rehearsal: launcher, seeds, barrier, max-over-ranks timing")
     ap.add_argument("--dry-step-ms", type=float, default=5.0,
                     help="dry run: rank r's stand-in step sleeps (r + 1) x this")
+    ap.add_argument("--dry-fail-rank", type=int, default=-1,
+                    help="dry run: this rank's stand-in verification fails (the job must report verified false)")
     return ap.parse_args(argv)
 
 
@@ -630,18 +659,40 @@ def dry_run(args, world: int, rank: int, local_rank: int) -> int:
         time.sleep(step)
     barrier()
     wall = time.perf_counter() - t0
+    chk_ok = rank != args.dry_fail_rank  # stand-in for the rank's oracle verification
+    t_job = reduce_max(wall, world)
     per_rank = gather({"rank": rank, "local_rank": local_rank, "world_size": int(os.environ.get("WORLD_SIZE", "1")),
                        "seed_base": rank_seed_base(rank), "wall_s": wall, "pid": os.getpid(),
                        "masks_head": erasure_masks(4, rank).tolist()}, world)
-    t_job = reduce_max(wall, world)
+    # host legs: stand-in records with the real records' shape (rank r moves
+    # (r + 1) GiB in (r + 1) x dry_step_ms per phase), assembled as run_rank does
+    barrier()
+    e0 = time.time()
+    time.sleep(step)
+    e1 = time.time()
+    time.sleep(step)
+    e2 = time.time()
+    gib = (rank + 1) * 2**30
+    e2e = {"stand_in": True, "raw": {"data_bytes": gib, "encode": [e0, e1], "decode": [e1, e2]}}
+    barrier()
+    w0 = time.time()
+    time.sleep(step)
+    mixed = {"stand_in": True, "verification": {"ok": chk_ok},
+             "raw": {"payload_bytes": gib, "e2e": [w0, time.time()], "device_s": step}}
+    e2e_all, mixed_all = gather(e2e, world), gather(mixed, world)
+    chk_ok = chk_ok and all(m["verification"]["ok"] for m in mixed_all)
+    extras = assemble_host_legs(e2e_all, mixed_all, world)
+    chk_ok = reduce_max(0.0 if chk_ok else 1.0, world) == 0.0
     if rank == 0:
         payload = 2 * S * K_DATA * L
-        print(json.dumps({"metric": "dry run (no GPU): launcher and control plane only", "dry_run": True,
-                          "value": round(job_throughput(payload, args.steps, world, t_job), 4), "unit": "GiB/s",
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": round(t_job / args.steps * 1e3, 4), "scaling": "weak",
-                          "rank_seed_bases": [r["seed_base"] for r in per_rank], "ranks": per_rank}), flush=True)
-    return 0
+        out = {"metric": "dry run (no GPU): launcher and control plane only", "dry_run": True,
+               "value": round(job_throughput(payload, args.steps, world, t_job), 4), "unit": "GiB/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(t_job / args.steps * 1e3, 4), "scaling": "weak", "verified": chk_ok,
+               "rank_seed_bases": [r["seed_base"] for r in per_rank], "ranks": per_rank}
+        out.update(extras)
+        print(json.dumps(out), flush=True)
+    return 0 if chk_ok else 3
 
 
 def run_rank(args, world: int, rank: int, local_rank: int) -> int:
@@ -753,17 +804,7 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
         e2e_all = gather(e2e, world)
         mixed_all = gather(mixed, world)
         chk_ok = chk_ok and all(m["verification"]["ok"] for m in mixed_all)
-        extras["end_to_end"] = e2e_all[0] if world == 1 else {
-            "aggregate": aggregate_host_path([r["raw"] for r in e2e_all]), "per_rank": e2e_all}
-        if world == 1:
-            extras["mixed"] = mixed_all[0]
-        else:
-            extras["mixed"] = {"per_rank": mixed_all,
-                               # one wall-clock window over every rank's end-to-end part
-                               "aggregate_end_to_end_data_GiB_s": round(
-                                   sum(m["raw"]["payload_bytes"] for m in mixed_all)
-                                   / (max(m["raw"]["e2e"][1] for m in mixed_all)
-                                      - min(m["raw"]["e2e"][0] for m in mixed_all)) / 2**30, 2)}
+        extras = assemble_host_legs(e2e_all, mixed_all, world)
 
     # every rank's verification counts (headline batch and mixed leg): the job
     # is verified only if all are

@@ -85,3 +85,77 @@ def test_host_path_aggregation():
     assert agg["decode_data_GiB_s"] == 40.0  # 20 GiB over 0.2 .. 0.7 s
     assert agg["per_rank_encode_data_GiB_s"] == [50.0, 25.0]
     assert agg["per_rank_decode_data_GiB_s"] == [40.0, 50.0]
+
+
+def test_eight_rank_dry_run_assembles_the_node_line():
+    """VERDICT r03 "next" 5: the driver's 8-GPU scaling run rehearsed without
+    hardware. 8 ranks through torch.distributed.run (gloo control plane):
+    max-over-ranks job time, every rank's record gathered on rank 0, and the
+    host legs' node aggregates (end_to_end.aggregate over the 8 ranks'
+    windows, mixed.aggregate_end_to_end_data_GiB_s) assembled by the same
+    function run_rank uses (bench.assemble_host_legs)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    steps, step_ms = 3, 10.0
+    r = _run(["--gpus", "8", "--dry-run", "--steps", str(steps), "--warmup", "1", "--dry-step-ms", str(step_ms)],
+             timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["verified"] is True
+    ranks = out["ranks"]
+    assert sorted(x["rank"] for x in ranks) == list(range(8))
+    assert len({x["pid"] for x in ranks}) == 8
+    assert out["rank_seed_bases"] == [bench.rank_seed_base(i) for i in range(8)]
+    slow = max(x["wall_s"] for x in ranks)  # rank 7: 8 x step_ms per step
+    assert out["ms_per_step"] == pytest.approx(slow / steps * 1e3, rel=0.05)
+    assert out["ms_per_step"] >= 8 * step_ms * 0.95
+    assert out["value"] == pytest.approx(bench.job_throughput(2 * 4096 * 10 * (1 << 20), steps, 8, slow), rel=0.05)
+    e2e = out["end_to_end"]
+    assert len(e2e["per_rank"]) == 8 and e2e["aggregate"]["ranks"] == 8
+    # the node aggregate is every rank's bytes over ONE window: below the sum
+    # of the per-rank rates (ranks overlap but are not simultaneous)
+    agg = e2e["aggregate"]["encode_data_GiB_s"]
+    assert 0 < agg <= sum(e2e["aggregate"]["per_rank_encode_data_GiB_s"]) * 1.001
+    assert agg == bench.aggregate_host_path([p["raw"] for p in e2e["per_rank"]])["encode_data_GiB_s"]
+    mixed = out["mixed"]
+    assert len(mixed["per_rank"]) == 8
+    window = (max(m["raw"]["e2e"][1] for m in mixed["per_rank"]) - min(m["raw"]["e2e"][0] for m in mixed["per_rank"]))
+    assert mixed["aggregate_end_to_end_data_GiB_s"] == pytest.approx(sum(range(1, 9)) / window, rel=0.02)
+
+
+def test_dry_run_one_failing_rank_fails_the_job():
+    """Verification is reduced over ranks: one rank's failed check makes the
+    job's line say verified false and every rank exit 3."""
+    r = _run(["--gpus", "4", "--dry-run", "--steps", "2", "--warmup", "0", "--dry-step-ms", "1",
+              "--dry-fail-rank", "2"], timeout=240)
+    assert r.returncode != 0
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert out["verified"] is False and out["n_gpus"] == 4
+
+
+def test_multi_gpu_leg_failures_are_records_not_exceptions():
+    """multi_gpu_e2e_child (the in-process multi-GPU host leg) turns every
+    failure of its child into a record: a time limit, a non-zero exit, output
+    that is not JSON, a child that cannot start. The headline line is
+    assembled around it either way."""
+    sys.path.insert(0, ROOT)
+    import bench
+    slow = bench.multi_gpu_e2e_child(2, timeout_s=0.5, cmd=[sys.executable, "-c", "import time; time.sleep(30)"])
+    assert slow == {"error": "timed out after 0 s"} or slow["error"].startswith("timed out")
+    bad = bench.multi_gpu_e2e_child(2, cmd=[sys.executable, "-c", "import sys; sys.stderr.write('boom'); sys.exit(4)"])
+    assert bad["error"] == "exit 4" and "boom" in bad["stderr_tail"]
+    junk = bench.multi_gpu_e2e_child(2, cmd=[sys.executable, "-c", "print('{not json')"])
+    assert junk["error"].startswith("unparsable output")
+    gone = bench.multi_gpu_e2e_child(2, cmd=["/nonexistent/python"])
+    assert gone["error"].startswith("could not start")
+    ok = bench.multi_gpu_e2e_child(2, cmd=[sys.executable, "-c", "import json; print(json.dumps({'devices': [0, 1]}))"])
+    assert ok == {"devices": [0, 1]}
+
+
+def test_assemble_host_legs_single_rank_passes_records_through():
+    sys.path.insert(0, ROOT)
+    import bench
+    e, m = {"raw": {"data_bytes": 1}}, {"raw": {"payload_bytes": 1, "e2e": [0, 1]}}
+    assert bench.assemble_host_legs([e], [m], 1) == {"end_to_end": e, "mixed": m}

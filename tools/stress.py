@@ -65,12 +65,18 @@ def main():
 
     def host_batch(rng):
         S, L = int(rng.integers(1, 9)), int(rng.choice([17, 4096, 65536, 1 << 20]))
-        t = torch.zeros((S, 14, L), dtype=torch.uint8)
-        if rng.integers(0, 2):
-            t = t.pin_memory()
+        devs = [0] * int(rng.integers(1, 4)) if rng.integers(0, 2) else None
+        kind = int(rng.integers(0, 3))  # pageable, torch-pinned, or a per-range placed batch
+        buf = None
+        if kind == 2 and devs is not None:
+            buf = H.HostBuffer.for_devices(devs, 14 * L, S)  # hec_host_alloc_multi
+            t = buf.tensor((S, 14, L))
+        else:
+            t = torch.zeros((S, 14, L), dtype=torch.uint8)
+            if kind:
+                t = t.pin_memory()
         a = t.numpy()
         a[:, :10] = rng.integers(0, 256, (S, 10, L), dtype=np.uint8)
-        devs = [0] * int(rng.integers(1, 4)) if rng.integers(0, 2) else None
         B.host_encode_batch(rs, t, devices=devs)
         assert np.array_equal(a[:, 10:], corc.encode_stripes(np.ascontiguousarray(a[:, :10]))), "host encode"
         want = a.copy()
@@ -81,7 +87,10 @@ def main():
                 a[s, int(i)] = 0x11
         assert B.host_reconstruct_batch(rs, t, masks, devices=devs) == 0
         assert np.array_equal(a, want), "host reconstruct"
-        note("host_batch" if devs is None else "host_batch_multi")
+        note("host_batch" if devs is None else ("host_batch_multi_placed" if buf else "host_batch_multi"))
+        if buf is not None:
+            del t, a
+            buf.close()
 
     def ragged(rng):
         n = int(rng.integers(1, 20))

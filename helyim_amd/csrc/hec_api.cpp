@@ -505,6 +505,26 @@ int Scratch::init() {
     return HEC_OK;
 }
 
+// Staging above kScratchKeep in a burst slot (index >= kWarmSlots) is freed
+// when its call ends: a burst of large per-call encodes (say 1 GiB shards:
+// 14 GiB of HBM each) must not stay resident in up to kScratchSlots slots for
+// the life of the process; the warm slots keep theirs.
+constexpr size_t kScratchKeep = size_t(64) << 20;
+void Scratch::trim_large() {
+    if (dcap <= kScratchKeep && hcap <= kScratchKeep) return;
+    (void)hipStreamSynchronize(stream);  // an error return may leave copies in flight
+    if (dcap > kScratchKeep) {
+        (void)hipFree(dbuf);
+        dbuf = nullptr;
+        dcap = 0;
+    }
+    if (hcap > kScratchKeep) {
+        (void)hipHostFree(hbuf);
+        hbuf = nullptr;
+        hcap = 0;
+    }
+}
+
 int lease_scratch(Lease<Scratch>& out) {
     int dev;
     int rc = current_device(&dev);
@@ -540,6 +560,7 @@ static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* co
     Lease<Scratch> lease;
     if ((rc = lease_scratch(lease))) return rc;
     Scratch* sc = lease.sc;
+    const ScratchTrim trim{sc, lease.index >= kWarmSlots};  // before the lease lets go
     const uint64_t Lp = round_up(L, 256);
     if ((rc = sc->reserve(size_t(Lp) * rs->n))) return rc;
     uint8_t* par = sc->dbuf + size_t(rs->k) * Lp;
@@ -618,6 +639,7 @@ static int reconstruct_host(const hec_rs* rs, uint8_t* const* shards, const size
     Lease<Scratch> lease;
     if ((rc = lease_scratch(lease))) return rc;
     Scratch* sc = lease.sc;
+    const ScratchTrim trim{sc, lease.index >= kWarmSlots};
     const uint64_t Lp = round_up(L, 256);
     if ((rc = sc->reserve(size_t(Lp) * rs->n))) return rc;
     HostPlans hp;

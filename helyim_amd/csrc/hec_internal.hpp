@@ -158,6 +158,18 @@ struct Scratch {
     int init();
     int reserve(size_t bytes);
     int reserve_host(size_t bytes);
+    void trim_large();  // free staging above 64 MiB (end of a call, slot still held)
+};
+// Slots created beyond the first kWarmSlots of a pool (bursts of concurrent
+// calls) free their large staging when their call ends, so the steady
+// footprint per device is that of kWarmSlots slots, not kScratchSlots.
+constexpr size_t kWarmSlots = 2;
+struct ScratchTrim {
+    Scratch* sc;
+    bool on;
+    ~ScratchTrim() {
+        if (on) sc->trim_large();
+    }
 };
 // Scratch slots per device: a host call leases one (its own stream, staging
 // buffers and completion flag), so concurrent calls from several threads

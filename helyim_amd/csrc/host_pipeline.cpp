@@ -110,11 +110,10 @@ struct Pipeline {
 // batches on one device -- other threads, or two ranges of one multi-device
 // call on the same GPU -- each lease their own streams and slots. Up to
 // kScratchSlots (8) pipelines exist per device, but only the first
-// kWarmPipelines keep their staging between calls: a pipeline created by a
+// kWarmSlots (2) keep their staging between calls: a pipeline created by a
 // burst of concurrent calls frees its large buffers when its call ends
 // (PipelineLease), so the steady footprint per device is that of two
 // pipelines (INTEGRATION.md §5 states the worst case).
-constexpr size_t kWarmPipelines = 2;
 std::mutex& pipeline_reg_mu() {
     static std::mutex* m = new std::mutex();
     return *m;
@@ -145,7 +144,7 @@ int lease_pipeline(PipelineLease& out) {
         pool = p.get();
     }
     if ((rc = pool->lease(out.lease))) return rc;
-    out.trim_after = out.lease.index >= kWarmPipelines;
+    out.trim_after = out.lease.index >= kWarmSlots;
     return HEC_OK;
 }
 

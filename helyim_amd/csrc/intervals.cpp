@@ -82,6 +82,24 @@ struct RaggedScratch {
         }
         return HEC_OK;
     }
+    // Compact staging above 64 MiB in a burst slot (index >= kWarmSlots) is
+    // freed when its call ends (ScratchTrim's rule, hec_internal.hpp).
+    void trim_large() {
+        constexpr size_t kKeep = size_t(64) << 20;
+        if (cap <= kKeep) return;
+        (void)hipStreamSynchronize(stream);  // an error return may leave copies in flight
+        (void)hipHostFree(host);
+        (void)hipFree(dev);
+        host = dev = nullptr;
+        cap = 0;
+    }
+};
+struct RaggedTrim {
+    RaggedScratch* sc;
+    bool on;
+    ~RaggedTrim() {
+        if (on) sc->trim_large();
+    }
 };
 
 // Per-device pool of ragged scratch slots (see SlotPool, hec_internal.hpp).
@@ -130,6 +148,7 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     Lease<RaggedScratch> lease;
     if ((rc = lease_ragged(lease))) return rc;
     RaggedScratch* sc = lease.sc;
+    const RaggedTrim trim{sc, lease.index >= kWarmSlots};  // before the lease lets go
     std::vector<RaggedItem> items(jobs.size());
     std::vector<uint32_t> block_item;
     for (size_t j = 0; j < jobs.size(); ++j) {

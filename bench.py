@@ -308,7 +308,10 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3, de
     import helyim_amd.batch as B
     dev = torch.empty((S, N_TOTAL, L), dtype=torch.uint8, device="cuda")
     B.fill_splitmix(dev, K_DATA * L, rank_seed_base(rank))
-    buf = H.HostBuffer(S * N_TOTAL * L)  # pinned, on this GPU's NUMA node
+    if devices is None:
+        buf = H.HostBuffer(S * N_TOTAL * L)  # pinned, on this GPU's NUMA node
+    else:  # one batch, each device's stripe range on that device's node
+        buf = H.HostBuffer.for_devices(devices, N_TOTAL * L, S)
     host = buf.tensor((S, N_TOTAL, L))
     host.copy_(dev)
     del dev
@@ -327,7 +330,9 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3, de
     node = buf.numa_node()
     del host
     buf.close()
-    return {"stripes": S, "shard_len": L, "host_memory": "pinned (hec_host_alloc: this GPU's NUMA node)",
+    mem = ("pinned (hec_host_alloc: this GPU's NUMA node)" if devices is None else
+           "pinned (hec_host_alloc_multi: each range on its GPU's NUMA node)")
+    return {"stripes": S, "shard_len": L, "host_memory": mem,
             "host_numa_node": node, "devices": devices if devices is not None else "current",
             "raw": {"data_bytes": data * reps, "encode": [enc0, enc1], "decode": [dec0, dec1]},
             "encode_data_GiB_s": round(data / te / 2**30, 2),

@@ -60,6 +60,7 @@ def test_bench_multi_gpu_host_leg_child():
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
     assert d["devices"] == [0, 0] and d["stripes"] == 512
+    assert "hec_host_alloc_multi" in d["host_memory"]  # each range on its GPU's NUMA node
     assert d["encode_data_GiB_s"] > 1 and d["decode_data_GiB_s"] > 1
 
 

@@ -193,7 +193,8 @@ static void check_batch(hec_rs_t* rs, void* ors) {
 /* hec_host_*_batch_multi: one [S][14][L] host batch split over the device
  * list {0,0,0} (three concurrent ranges on one GPU, each on its own host
  * thread and pipeline; an 8-GPU server lists 0..7), once in pageable memory
- * (pooled pinned staging) and once in hec_host_alloc'd memory (zero copy);
+ * (pooled pinned staging), in hec_host_alloc'd memory and in one
+ * hec_host_alloc_multi batch (ranges placed per device; both zero copy);
  * parity and a 0..5-erasure reconstruct against the C oracle. */
 static void check_host_batch_multi(void* ors) {
     enum { S = 11 };
@@ -201,9 +202,11 @@ static void check_host_batch_multi(void* ors) {
     const int devs[3] = {0, 0, 0};
     hec_rs_t* rs = NULL;
     CHECK(hec_rs_new(K, M, &rs) == HEC_OK, "new");
-    for (int pinned = 0; pinned < 2; ++pinned) {
+    for (int pinned = 0; pinned < 3; ++pinned) {  /* pageable, hec_host_alloc, hec_host_alloc_multi */
         uint8_t* h = NULL;
-        if (pinned) CHECK(hec_host_alloc(S * stripe, (void**)&h) == HEC_OK && h, "host_alloc");
+        if (pinned == 1) CHECK(hec_host_alloc(S * stripe, (void**)&h) == HEC_OK && h, "host_alloc");
+        else if (pinned == 2)
+            CHECK(hec_host_alloc_multi(devs, 3, stripe, S, (void**)&h) == HEC_OK && h, "host_alloc_multi");
         else h = malloc(S * stripe);
         if (!h) return;
         uint8_t* want = malloc(S * stripe);

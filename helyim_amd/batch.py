@@ -198,6 +198,16 @@ def reconstruct_ragged(rs: ReedSolomon, base: torch.Tensor, descs, bad_stripes: 
                                          _stream_ptr(stream)))
 
 
+def host_zero_copy(t: torch.Tensor) -> bool:
+    """True when host batches on t's bytes are coded zero-copy on the current
+    device (hec_host_zero_copy_view): t is one pinned, GPU-addressable range."""
+    import ctypes
+    z = ctypes.c_int(0)
+    span = (t.numel() and (sum((n - 1) * st for n, st in zip(t.shape, t.stride())) + 1)) * t.element_size()
+    check(lib.hec_host_zero_copy_view(t.data_ptr(), span, ctypes.byref(z)))
+    return bool(z.value)
+
+
 def ragged_kernel_name(descs, decode: bool) -> str:
     """The kernel (and workgroup order) encode_ragged / reconstruct_ragged runs
     on these descriptors under the current knobs (hec_ragged_kernel_name: the

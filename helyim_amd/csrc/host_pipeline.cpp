@@ -562,6 +562,18 @@ int hec_host_reconstruct_batch_multi(const hec_rs_t* rs, const int* devices, siz
     return HEC_OK;
 }
 
+int hec_host_zero_copy_view(const void* p, uint64_t bytes, int* zero_copy) {
+    if (!zero_copy) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
+    *zero_copy = 0;
+    if (!p || bytes == 0) return HEC_OK;
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    uint8_t* d = nullptr;
+    *zero_copy = host_device_view(p, bytes, &d) ? 1 : 0;
+    return HEC_OK;
+}
+
 int hec_host_staging_stats(int* n_pipelines, uint64_t* pinned_bytes, uint64_t* device_bytes) {
     int dev;
     int rc = current_device(&dev);

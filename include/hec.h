@@ -451,6 +451,12 @@ int hec_set_host_staging(uint64_t max_bytes);
 /* Host batches on pinned memory: 1 = zero-copy kernels (default), 0 = the
  * copy pipeline. Speed only; identical results. Returns HEC_OK. */
 int hec_set_host_zero_copy(int on);
+/* Diagnostic: *zero_copy = 1 when [p, p + bytes) is one pinned range the
+ * current device can address, i.e. host batches on it are coded zero-copy
+ * (hec_host_alloc, hec_host_alloc_multi, hipHostMalloc, torch pin_memory),
+ * 0 when they go through staging copies (pageable memory), or with
+ * hec_set_host_zero_copy(0). */
+int hec_host_zero_copy_view(const void* p, uint64_t bytes, int* zero_copy);
 /* Diagnostic: host-batch pipelines of the current device (at most 8; only
  * the first 2 keep their staging between calls, the others free it when
  * their call ends) and the pinned host / device staging bytes they hold now.

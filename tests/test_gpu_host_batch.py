@@ -327,3 +327,28 @@ def test_host_pipeline_pool_trims_after_a_burst(gpu, host_path):
     assert pinned.value <= 2 * per_pinned, (n.value, pinned.value)
     assert dev.value <= 2 * per_dev, (n.value, dev.value)
     torch.cuda.synchronize()
+
+
+def test_which_buffers_are_coded_zero_copy(gpu, host_path):
+    """hec_host_zero_copy_view: hec_host_alloc, hec_host_alloc_multi
+    (hipHostRegister'd, not hipHostMalloc'd) and torch pinned buffers are
+    coded in place over PCIe; pageable memory, a range running past a pinned
+    allocation, and everything under hec_set_host_zero_copy(0) take staging."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    on = host_path == "zero_copy"
+    S, L = 4, 4096
+    a = H.HostBuffer(S * 14 * L)
+    b = H.HostBuffer.for_devices([0, 0], 14 * L, S)
+    ta, tb = a.tensor((S, 14, L)), b.tensor((S, 14, L))
+    tp = torch.zeros((S, 14, L), dtype=torch.uint8).pin_memory()
+    tq = torch.zeros((S, 14, L), dtype=torch.uint8)
+    assert B.host_zero_copy(ta) == on and B.host_zero_copy(tb) == on and B.host_zero_copy(tp) == on
+    assert not B.host_zero_copy(tq)
+    z = ctypes_int = __import__("ctypes").c_int(7)
+    assert H.lib.hec_host_zero_copy_view(a.ptr, S * 14 * L + (1 << 30), __import__("ctypes").byref(z)) == 0
+    assert ctypes_int.value == 0  # runs past the allocation
+    del ta, tb
+    a.close()
+    b.close()

@@ -334,6 +334,7 @@ def test_which_buffers_are_coded_zero_copy(gpu, host_path):
     (hipHostRegister'd, not hipHostMalloc'd) and torch pinned buffers are
     coded in place over PCIe; pageable memory, a range running past a pinned
     allocation, and everything under hec_set_host_zero_copy(0) take staging."""
+    import ctypes
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -346,9 +347,9 @@ def test_which_buffers_are_coded_zero_copy(gpu, host_path):
     tq = torch.zeros((S, 14, L), dtype=torch.uint8)
     assert B.host_zero_copy(ta) == on and B.host_zero_copy(tb) == on and B.host_zero_copy(tp) == on
     assert not B.host_zero_copy(tq)
-    z = ctypes_int = __import__("ctypes").c_int(7)
-    assert H.lib.hec_host_zero_copy_view(a.ptr, S * 14 * L + (1 << 30), __import__("ctypes").byref(z)) == 0
-    assert ctypes_int.value == 0  # runs past the allocation
+    z = ctypes.c_int(7)
+    assert H.lib.hec_host_zero_copy_view(a.ptr, S * 14 * L + (1 << 30), ctypes.byref(z)) == 0
+    assert z.value == 0  # runs past the allocation
     del ta, tb
     a.close()
     b.close()

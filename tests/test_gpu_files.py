@@ -292,3 +292,23 @@ def test_reference_geometry_large_row_threshold(gpu, extra):
             assert _same_file(a + H.to_ext(i), b + O.to_ext(i)), i
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+def test_write_error_in_the_pipeline_carries_its_errno(gpu, tmp_path):
+    """An I/O error inside the file pipeline's writer threads (encoder.rs:194
+    `output.write_all(..)?` -> EcShardError::Io) comes back with its errno:
+    shard 3's output is /dev/full, so its pwritev fails with ENOSPC after the
+    GPU coded the rows, and hec_last_error_values carries 28 out of the
+    worker thread (ErrorSlot -> drain)."""
+    import errno
+    import helyim_amd as H
+    if not os.path.exists("/dev/full"):
+        pytest.skip("no /dev/full")
+    base = str(tmp_path / "v")
+    open(base + ".dat", "wb").write(O.synthetic_volume(3_000_000).tobytes())
+    os.symlink("/dev/full", base + H.to_ext(3))
+    with pytest.raises(H.Io) as ei:
+        H.write_ec_files(base)
+    assert ei.value.errno == errno.ENOSPC, (ei.value.errno, str(ei.value))
+    assert isinstance(ei.value.os_error, OSError) and ei.value.os_error.errno == errno.ENOSPC
+    assert "(os error 28)" in str(ei.value)

@@ -282,7 +282,7 @@ int decode_plan(const hec_rs* rs, const uint8_t* present, bool data_only, Mat& c
         *noop = true;
         return HEC_OK;
     }
-    if (npresent < k) return HEC_ERR_TOO_FEW_SHARDS_PRESENT;
+    if (npresent < k) return fail(HEC_ERR_TOO_FEW_SHARDS_PRESENT, "");
     std::vector<uint32_t> miss;
     for (int i = 0; i < n; ++i) {
         if (present[i]) {
@@ -544,11 +544,11 @@ static uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // upstream check_piece_count!(all) + check_slices!(multi)
 static int check_shards(const hec_rs* rs, const void* shards, const size_t* lens, size_t n_shards) {
     if (!shards || !lens) return fail(HEC_ERR_INVALID_ARGUMENT, "null shards");
-    if (n_shards < size_t(rs->n)) return HEC_ERR_TOO_FEW_SHARDS;
-    if (n_shards > size_t(rs->n)) return HEC_ERR_TOO_MANY_SHARDS;
-    if (lens[0] == 0) return HEC_ERR_EMPTY_SHARD;
+    if (n_shards < size_t(rs->n)) return fail(HEC_ERR_TOO_FEW_SHARDS, "");
+    if (n_shards > size_t(rs->n)) return fail(HEC_ERR_TOO_MANY_SHARDS, "");
+    if (lens[0] == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
     for (size_t i = 1; i < n_shards; ++i)
-        if (lens[i] != lens[0]) return HEC_ERR_INCORRECT_SHARD_SIZE;
+        if (lens[i] != lens[0]) return fail(HEC_ERR_INCORRECT_SHARD_SIZE, "");
     return HEC_OK;
 }
 
@@ -612,19 +612,19 @@ static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* co
 static int reconstruct_host(const hec_rs* rs, uint8_t* const* shards, const size_t* lens,
                             const uint8_t* present, size_t n_shards, bool data_only) {
     if (!shards || !lens || !present) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    if (n_shards < size_t(rs->n)) return HEC_ERR_TOO_FEW_SHARDS;
-    if (n_shards > size_t(rs->n)) return HEC_ERR_TOO_MANY_SHARDS;
+    if (n_shards < size_t(rs->n)) return fail(HEC_ERR_TOO_FEW_SHARDS, "");
+    if (n_shards > size_t(rs->n)) return fail(HEC_ERR_TOO_MANY_SHARDS, "");
     size_t L = 0;
     int npresent = 0;
     for (size_t i = 0; i < n_shards; ++i) {
         if (!present[i]) continue;
-        if (lens[i] == 0) return HEC_ERR_EMPTY_SHARD;
-        if (npresent && lens[i] != L) return HEC_ERR_INCORRECT_SHARD_SIZE;
+        if (lens[i] == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
+        if (npresent && lens[i] != L) return fail(HEC_ERR_INCORRECT_SHARD_SIZE, "");
         L = lens[i];
         ++npresent;
     }
     if (npresent == rs->n) return HEC_OK;
-    if (npresent < rs->k) return HEC_ERR_TOO_FEW_SHARDS_PRESENT;
+    if (npresent < rs->k) return fail(HEC_ERR_TOO_FEW_SHARDS_PRESENT, "");
     if (rs->k == 10 && rs->m == 4 && uint64_t(rs->k) * L <= host_staging_max())
         // one-stripe degraded read: pinned compact staging + the dense-LUT kernel
         return hec_rs_reconstruct_batch(rs, shards, lens, present, 1, data_only ? 1 : 0, nullptr);
@@ -814,9 +814,9 @@ int hec_set_kernel_mode(int mode) {
 int hec_rs_new(size_t data_shards, size_t parity_shards, hec_rs_t** out) {
     if (!out) return fail(HEC_ERR_INVALID_ARGUMENT, "null out");
     *out = nullptr;
-    if (data_shards == 0) return HEC_ERR_TOO_FEW_DATA_SHARDS;
-    if (parity_shards == 0) return HEC_ERR_TOO_FEW_PARITY_SHARDS;
-    if (data_shards + parity_shards > 256) return HEC_ERR_TOO_MANY_SHARDS;
+    if (data_shards == 0) return fail(HEC_ERR_TOO_FEW_DATA_SHARDS, "");
+    if (parity_shards == 0) return fail(HEC_ERR_TOO_FEW_PARITY_SHARDS, "");
+    if (data_shards + parity_shards > 256) return fail(HEC_ERR_TOO_MANY_SHARDS, "");
     hec_rs_t* rs = new hec_rs_t();
     rs->k = int(data_shards);
     rs->m = int(parity_shards);
@@ -875,7 +875,7 @@ int hec_gpu_encode_batch(const hec_rs_t* rs, const uint8_t* d_data, uint64_t dat
                          uint64_t data_shard_stride, uint8_t* d_parity, uint64_t parity_stripe_stride,
                          uint64_t parity_shard_stride, uint64_t shard_len, uint32_t n_stripes, void* stream) {
     if (!rs || !d_data || !d_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
     int rc;
     if ((rc = check_strided("data", uint32_t(rs->k), data_stripe_stride, data_shard_stride, shard_len, n_stripes)) ||
         (rc = check_strided("parity", uint32_t(rs->m), parity_stripe_stride, parity_shard_stride, shard_len,
@@ -892,7 +892,7 @@ int hec_gpu_reconstruct_batch(const hec_rs_t* rs, uint8_t* d_shards, uint64_t st
                               uint64_t shard_len, uint32_t n_stripes, const uint32_t* d_present_masks,
                               uint32_t* d_bad_stripes, void* stream) {
     if (!rs || !d_shards || !d_present_masks) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
     int rc;
     if ((rc = check_strided("shards", uint32_t(rs->n), stripe_stride, shard_stride, shard_len, n_stripes))) return rc;
     GeomDevice* gd;

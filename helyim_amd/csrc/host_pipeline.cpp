@@ -272,7 +272,7 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
                           uint64_t data_shard_stride, uint8_t* h_parity, uint64_t parity_stripe_stride,
                           uint64_t parity_shard_stride, uint64_t shard_len, uint32_t n_stripes) {
     if (!rs || !h_data || !h_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
     if (n_stripes == 0) return HEC_OK;
     int rc;
     if ((rc = check_strided("data", uint32_t(rs->k), data_stripe_stride, data_shard_stride, shard_len, n_stripes)) ||
@@ -368,7 +368,7 @@ int hec_host_reconstruct_batch(const hec_rs_t* rs, uint8_t* h_shards, uint64_t s
                                uint64_t shard_len, uint32_t n_stripes, const uint32_t* h_present_masks,
                                uint32_t* n_bad_stripes) {
     if (!rs || !h_shards || !h_present_masks) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
     if (n_bad_stripes) *n_bad_stripes = 0;
     if (n_stripes == 0) return HEC_OK;
     int rc;
@@ -530,7 +530,7 @@ int hec_host_encode_batch_multi(const hec_rs_t* rs, const int* devices, size_t n
                                 uint64_t parity_stripe_stride, uint64_t parity_shard_stride, uint64_t shard_len,
                                 uint32_t n_stripes) {
     if (!rs || !h_data || !h_parity) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
     int rc;
     if ((rc = check_strided("data", uint32_t(rs->k), data_stripe_stride, data_shard_stride, shard_len, n_stripes)) ||
         (rc = check_strided("parity", uint32_t(rs->m), parity_stripe_stride, parity_shard_stride, shard_len,
@@ -547,7 +547,7 @@ int hec_host_reconstruct_batch_multi(const hec_rs_t* rs, const int* devices, siz
                                      uint64_t stripe_stride, uint64_t shard_stride, uint64_t shard_len,
                                      uint32_t n_stripes, const uint32_t* h_present_masks, uint32_t* n_bad_stripes) {
     if (!rs || !h_shards || !h_present_masks) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
-    if (shard_len == 0) return HEC_ERR_EMPTY_SHARD;
+    if (shard_len == 0) return fail(HEC_ERR_EMPTY_SHARD, "");
     if (n_bad_stripes) *n_bad_stripes = 0;
     int rc;
     if ((rc = check_strided("shards", uint32_t(rs->n), stripe_stride, shard_stride, shard_len, n_stripes))) return rc;

@@ -269,7 +269,7 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
                     err = fail(HEC_ERR_INVALID_ARGUMENT, "missing shard without a buffer");
         if (err) {
             if (bad_index) *bad_index = s;
-            return err;
+            return err == HEC_ERR_INVALID_ARGUMENT ? err : fail(err, "stripe " + std::to_string(s));
         }
         if (np == n) continue;  // upstream no-op
         act.push_back({s, L, mask});

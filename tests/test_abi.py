@@ -346,3 +346,20 @@ def test_host_alloc_multi_arguments_checked_before_device():
     many = (ctypes.c_int * 257)()
     assert lib.hec_host_alloc_multi(many, 257, 4096, 4, ctypes.byref(p)) == 66
     assert p.value is None
+
+
+def test_every_failure_resets_the_detail_and_values(tmp_path):
+    """hec_last_error_detail / _values describe the LAST failure: an RS-level
+    error after an Io failure leaves neither the old text nor the old errno."""
+    import helyim_amd as H
+    from helyim_amd import _lib
+    with pytest.raises(H.Io):
+        H.write_ec_files(str(tmp_path / "missing"))
+    assert _lib.last_detail() and _lib.last_values()[2] == 2
+    rs = H.ReedSolomon(10, 4)
+    with pytest.raises(H.TooFewShards):
+        rs.encode([np.zeros(8, np.uint8) for _ in range(13)])
+    assert _lib.last_detail() == "" and _lib.last_values() == (0, 0, 0)
+    with pytest.raises(H.TooFewShardsPresent):
+        rs.reconstruct_batch([[np.zeros(8, np.uint8)] * 14, [None] * 5 + [np.zeros(8, np.uint8)] * 9])
+    assert _lib.last_detail() == "stripe 1"

@@ -10,7 +10,10 @@ survivors and rewrites its 4 erased shards). Inputs are synthetic splitmix64
 stripes generated in HBM before the timed region.
 
 value = data-payload GiB/s over all ranks: (encode 10*L + decode 10*L bytes
-per stripe) * stripes * ranks / max-over-ranks step time. Multi-GPU: one
+per stripe) * stripes * ranks / max-over-ranks step time. After the timed
+region (outside the clock) every rank checks its WHOLE batch against the C
+oracle (oracle/corc.py: data, parity and the rebuilt shards of every stripe)
+and its mixed leg's stripes; `verified` is the AND over ranks. Multi-GPU: one
 process per GPU, independent stripe batches per rank (seed base
 0x5EED0000 + rank*2^20), no data-path collective ("scaling": "weak"); the
 only cross-rank traffic is the barrier and the max-reduce of the timings

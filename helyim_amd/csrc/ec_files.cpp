@@ -176,6 +176,11 @@ bool pwritev_all(int fd, std::vector<iovec> iov, uint64_t off, ErrorSlot& e) {
             io_error(e, "write");
             return false;
         }
+        if (w == 0) {  // no progress on a non-empty write: fail instead of spinning (write_all's WriteZero)
+            errno = EIO;
+            io_error(e, "write: wrote zero bytes");
+            return false;
+        }
         off += uint64_t(w);
         while (w > 0 && first < iov.size()) {
             if (size_t(w) >= iov[first].iov_len) {

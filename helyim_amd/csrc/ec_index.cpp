@@ -67,11 +67,24 @@ bool read_all(int fd, std::vector<uint8_t>& out) {
     return true;
 }
 
+// One pwrite of exactly n bytes; a short write is an error with errno EIO
+// (errno is otherwise left from some earlier call).
+bool pwrite_exact(int fd, const void* p, size_t n, off_t off) {
+    const ssize_t w = ::pwrite(fd, p, n, off);
+    if (w == ssize_t(n)) return true;
+    if (w >= 0) errno = EIO;
+    return false;
+}
+
 bool write_all(int fd, const uint8_t* p, size_t n) {
     while (n) {
         ssize_t w = ::write(fd, p, n);
         if (w < 0) {
             if (errno == EINTR) continue;
+            return false;
+        }
+        if (w == 0) {  // no progress: fail (write_all's WriteZero) instead of spinning
+            errno = EIO;
             return false;
         }
         p += w;
@@ -181,7 +194,7 @@ int hec_rebuild_ecx_file(const char* base_filename) {
             if (r != ssize_t(kEntry)) return r < 0 ? io("read .ecx") : eof("read .ecx");
             const uint64_t key = be64(e);
             if (key == want) {
-                if (::pwrite(ecx.fd, tomb, 4, off_t(mid * 16 + 8 + 4)) != 4) return io("write .ecx");
+                if (!pwrite_exact(ecx.fd, tomb, 4, off_t(mid * 16 + 8 + 4))) return io("write .ecx");
                 break;
             }
             if (key < want)

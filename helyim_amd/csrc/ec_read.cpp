@@ -35,6 +35,14 @@ constexpr uint64_t kEntry = 16;  // NEEDLE_ENTRY_SIZE
 
 int io(const std::string& what) { return fail_errno(HEC_ERR_IO, what, errno); }
 
+// One pwrite of exactly n bytes; a short write is an error with errno EIO.
+bool pwrite_exact(int fd, const void* p, size_t n, off_t off) {
+    const ssize_t w = ::pwrite(fd, p, n, off);
+    if (w == ssize_t(n)) return true;
+    if (w >= 0) errno = EIO;
+    return false;
+}
+
 uint64_t be64(const uint8_t* p) {
     uint64_t v = 0;
     for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
@@ -542,12 +550,12 @@ int hec_ec_volume_delete_needle(hec_ec_volume_t* vol, uint64_t needle_id) {
     if (rc < 0) return fail(HEC_ERR_IO, "Needle " + std::to_string(needle_id) + " is not found");
     if (rc) return rc;
     const uint8_t tomb[4] = {0xFF, 0xFF, 0xFF, 0xFF};  // TOMBSTONE_FILE_SIZE = -1, big-endian
-    if (::pwrite(vol->ecx.fd, tomb, 4, off_t(entry * kEntry + 12)) != 4) return io("write " + vol->ecx.name);
+    if (!pwrite_exact(vol->ecx.fd, tomb, 4, off_t(entry * kEntry + 12))) return io("write " + vol->ecx.name);
     struct stat st;
     if (::fstat(vol->ecj_fd, &st) != 0) return io("stat " + vol->base + ".ecj");
     uint8_t id[8];
     for (int i = 0; i < 8; ++i) id[i] = uint8_t(needle_id >> (56 - 8 * i));
-    if (::pwrite(vol->ecj_fd, id, 8, st.st_size) != 8) return io("write " + vol->base + ".ecj");
+    if (!pwrite_exact(vol->ecj_fd, id, 8, st.st_size)) return io("write " + vol->base + ".ecj");
     return HEC_OK;
 }
 

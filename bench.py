@@ -344,6 +344,30 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3, de
             "decode_pcie_GB_s": round(S * N_TOTAL * L / td / 1e9, 2)}
 
 
+MIXED_LENS = [(64 << 10) << i for i in range(7)]  # 64 KiB .. 4 MiB
+
+
+def mixed_workload(rank: int, n_stripes: int):
+    """BASELINE config 5, seeded per rank: shard lengths log-uniform over
+    64 KiB..4 MiB, 0..4 erasures per stripe (uniform count, uniform shards).
+    Stripes packed back to back (shard stride = length); stripe s's data is
+    splitmix64(rank_seed_base(rank) + s). -> (lengths, erasure counts, present
+    masks, hec_stripe_desc rows, total bytes)."""
+    rng = np.random.default_rng(0x5E + rank)
+    Ls = rng.choice(MIXED_LENS, n_stripes)
+    es = rng.integers(0, 5, n_stripes)
+    full = (1 << N_TOTAL) - 1
+    masks = np.empty(n_stripes, dtype=np.int64)
+    for s in range(n_stripes):
+        drop = rng.choice(N_TOTAL, int(es[s]), replace=False)
+        masks[s] = full & ~int(sum(1 << int(i) for i in drop))
+    descs, off = [], 0
+    for s in range(n_stripes):
+        descs.append((off, int(Ls[s]), int(Ls[s]), int(masks[s])))
+        off += N_TOTAL * int(Ls[s])
+    return Ls, es, masks, descs, off
+
+
 def mixed_section(rs, rank: int, n_stripes: int = 2048, e2e_stripes: int = 512) -> dict:
     """BASELINE config 5: shard lengths 64 KiB..4 MiB (log-uniform), 0..4
     erasures per stripe. Device-resident: all n_stripes packed in one HBM
@@ -355,19 +379,9 @@ def mixed_section(rs, rank: int, n_stripes: int = 2048, e2e_stripes: int = 512) 
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
-    rng = np.random.default_rng(0x5E + rank)
-    lens = [(64 << 10) << i for i in range(7)]
-    Ls = rng.choice(lens, n_stripes)
-    es = rng.integers(0, 5, n_stripes)
+    lens = MIXED_LENS
+    Ls, es, masks, descs, off = mixed_workload(rank, n_stripes)
     full = (1 << N_TOTAL) - 1
-    masks = np.empty(n_stripes, dtype=np.int64)
-    for s in range(n_stripes):
-        drop = rng.choice(N_TOTAL, int(es[s]), replace=False)
-        masks[s] = full & ~int(sum(1 << int(i) for i in drop))
-    descs, off = [], 0
-    for s in range(n_stripes):
-        descs.append((off, int(Ls[s]), int(Ls[s]), int(masks[s])))
-        off += N_TOTAL * int(Ls[s])
     dev = torch.empty(off, dtype=torch.uint8, device="cuda")
     for s, (o, st, L, _) in enumerate(descs):
         B.fill_splitmix(dev[o:o + K_DATA * L].view(1, 1, -1), K_DATA * L, rank_seed_base(rank) + s)

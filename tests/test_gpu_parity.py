@@ -1105,3 +1105,60 @@ def test_ragged_and_batched_reconstruct_every_pattern(gpu):
     for j, s in enumerate(stripes):
         for i in range(14):
             assert np.array_equal(s[i], full[j][i]), (pats[j], i)
+
+
+def _check_ragged_all(dev, descs, seeds, masks=None, group=32):
+    """Every stripe of a packed ragged device batch against the C oracle
+    (corc.check_stripes), stripes of one length copied back `group` at a time.
+    -> indices of the stripes that differ."""
+    by_len = {}
+    for s, (_, _, L, _) in enumerate(descs):
+        by_len.setdefault(L, []).append(s)
+    bad = []
+    for L, idx in by_len.items():
+        for g in range(0, len(idx), group):
+            sel = idx[g:g + group]
+            host = np.stack([dev[descs[s][0]:descs[s][0] + 14 * L].view(14, L).cpu().numpy() for s in sel])
+            m = None if masks is None else np.array([masks[s] for s in sel], dtype=np.int64)
+            sd = np.array([seeds[s] for s in sel], dtype=np.uint64)
+            bad += [sel[j] for j in corc.check_stripes(host, m, 16, sd)]
+    return sorted(bad)
+
+
+def test_config5_whole_batch_vs_oracle(gpu):
+    """BASELINE config 5 exactly as the bench runs it (bench.mixed_workload:
+    2048 stripes, 64 KiB..4 MiB, 0..4 erasures, 32 GiB in HBM), EVERY stripe
+    against the C oracle: after one ragged encode launch, data and parity of
+    all 2048 stripes; then every erased shard overwritten, one ragged
+    reconstruct launch, and all stripes again (rebuilt shards = the oracle's
+    reconstruct from the same survivors). The bench's own mixed leg checks a
+    64-stripe sample after its timed launches."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    import bench
+    rs = H.ReedSolomon(10, 4)
+    Ls, es, masks, descs, off = bench.mixed_workload(0, 2048)
+    seeds = [bench.rank_seed_base(0) + s for s in range(len(descs))]
+    torch.cuda.empty_cache()
+    dev = torch.empty(off, dtype=torch.uint8, device="cuda")
+    for s, (o, _, L, _) in enumerate(descs):
+        B.fill_splitmix(dev[o:o + 10 * L].view(1, 1, -1), 10 * L, seeds[s])
+    darr = np.array(descs, dtype=B.desc_dtype())
+    B.encode_ragged(rs, dev, darr)
+    torch.cuda.synchronize()
+    assert _check_ragged_all(dev, descs, seeds) == []
+    erased = 0
+    for (o, _, L, m) in descs:
+        for i in range(14):
+            if not (m >> i) & 1:
+                dev[o + i * L:o + (i + 1) * L].fill_(0xA5)
+                erased += 1
+    assert erased == int(sum(es))
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.reconstruct_ragged(rs, dev, darr, bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0
+    assert _check_ragged_all(dev, descs, seeds, masks) == []
+    del dev
+    torch.cuda.empty_cache()

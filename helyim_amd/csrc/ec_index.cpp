@@ -67,14 +67,6 @@ bool read_all(int fd, std::vector<uint8_t>& out) {
     return true;
 }
 
-// One pwrite of exactly n bytes; a short write is an error with errno EIO
-// (errno is otherwise left from some earlier call).
-bool pwrite_exact(int fd, const void* p, size_t n, off_t off) {
-    const ssize_t w = ::pwrite(fd, p, n, off);
-    if (w == ssize_t(n)) return true;
-    if (w >= 0) errno = EIO;
-    return false;
-}
 
 bool write_all(int fd, const uint8_t* p, size_t n) {
     while (n) {

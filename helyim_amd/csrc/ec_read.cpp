@@ -35,13 +35,6 @@ constexpr uint64_t kEntry = 16;  // NEEDLE_ENTRY_SIZE
 
 int io(const std::string& what) { return fail_errno(HEC_ERR_IO, what, errno); }
 
-// One pwrite of exactly n bytes; a short write is an error with errno EIO.
-bool pwrite_exact(int fd, const void* p, size_t n, off_t off) {
-    const ssize_t w = ::pwrite(fd, p, n, off);
-    if (w == ssize_t(n)) return true;
-    if (w >= 0) errno = EIO;
-    return false;
-}
 
 uint64_t be64(const uint8_t* p) {
     uint64_t v = 0;

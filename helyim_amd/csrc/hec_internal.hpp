@@ -2,9 +2,11 @@
 // (ec_files.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -58,6 +60,15 @@ inline int check_strided(const char* what, uint32_t shards, uint64_t stripe_stri
     return HEC_OK;
 }
 int hip_fail(hipError_t e, const char* what);
+
+// One pwrite of exactly n bytes (the .ecx tombstone, the .ecj append); a
+// short write is an error with errno EIO (errno would otherwise be stale).
+inline bool pwrite_exact(int fd, const void* p, size_t n, off_t off) {
+    const ssize_t w = ::pwrite(fd, p, n, off);
+    if (w == ssize_t(n)) return true;
+    if (w >= 0) errno = EIO;
+    return false;
+}
 
 // Propagate a non-zero hec status.
 #define HEC_TRY(call)            \

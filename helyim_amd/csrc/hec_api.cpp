@@ -68,8 +68,14 @@ int hip_fail(hipError_t e, const char* what) {
 namespace {
 class HostPool {
    public:
-    explicit HostPool(unsigned n) {
-        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    // Workers of device `dev`'s pool run on that GPU's NUMA node (when the
+    // platform says which; they copy into and out of its pinned staging).
+    HostPool(unsigned n, int dev) {
+        for (unsigned i = 0; i < n; ++i)
+            th_.emplace_back([this, dev] {
+                (void)hec_bind_thread_to_device(dev, nullptr);  // placement only: no-op when unknown
+                loop();
+            });
     }
     // false if another caller owns the pool (run serially then)
     bool run(size_t n, unsigned max_threads, const std::function<void(size_t)>& fn) {
@@ -140,9 +146,8 @@ class HostPool {
 // never destroyed: their threads live for the process). A call takes a free
 // pool of its current device, so the ranges of one multi-device host call --
 // and concurrent callers on different GPUs -- copy on their own workers
-// instead of all but one running serially. A pool's threads
-// inherit the CPU affinity of the thread that created it: a range thread
-// bound to its GPU's NUMA node (run_device_ranges) gets workers on that node.
+// instead of all but one running serially. Each pool's workers
+// bind themselves to their device's NUMA node, whichever thread created it.
 constexpr size_t kPoolsPerDevice = 2;
 void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>& fn) {
     static std::mutex mu;
@@ -164,7 +169,7 @@ void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>&
         std::lock_guard<std::mutex> lk(mu);
         auto& v = (*pools)[dev];
         if (v.size() < kPoolsPerDevice) {
-            fresh = new HostPool(15);
+            fresh = new HostPool(15, dev);
             v.push_back(fresh);
         }
     }

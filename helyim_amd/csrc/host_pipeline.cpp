@@ -216,8 +216,8 @@ int run_device_ranges(const int* devices, size_t n_devices, uint32_t n_stripes,
             return fail(HEC_ERR_INVALID_ARGUMENT,
                         "device " + std::to_string(devices[r]) + " of " + std::to_string(count) + " in the list");
     if (n_stripes == 0) return HEC_OK;
-    // (Each device's host worker pools start on first use from a range thread
-    // already bound to that GPU's node, so their workers copy on that node.)
+    // (Each device's host worker pools bind their workers to that GPU's node,
+    // so a range's staging copies run next to its pinned memory.)
     const size_t R = std::min<size_t>(n_devices, n_stripes);
     std::vector<int> rcs(R, HEC_OK);
     std::vector<std::string> details(R);

@@ -199,3 +199,38 @@ def test_multi_device_batch_pages_follow_their_ranges(monkeypatch):
     assert buf.numa_node_at(0) == a and buf.numa_node_at(S * stride - 1) == b
     del t
     buf.close()
+
+
+def test_host_worker_pool_threads_sit_on_the_gpus_node():
+    """Each device's host worker pool binds its workers to that GPU's NUMA
+    node (hec_api.cpp HostPool), whichever thread first needed it: after a
+    pageable host batch (staging copies on the pool), at least the 15 workers
+    of device 0's pool run on exactly the CPUs hec_bind_thread_to_device(0)
+    gives a thread here."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    res = {}
+
+    def probe():  # a fresh thread: what binding to device 0 yields here
+        res["info"] = H.bind_host_to_device(0)
+        res["cpus"] = os.sched_getaffinity(0)
+
+    t = threading.Thread(target=probe)
+    t.start()
+    t.join()
+    if not res["info"]["bound_cpus"] or res["cpus"] == os.sched_getaffinity(0):
+        pytest.skip(f"binding to device 0's node changes nothing here ({res['info']})")
+    torch.cuda.set_device(0)
+    S, L = 16, 1 << 20
+    host = torch.zeros((S, 14, L), dtype=torch.uint8)  # pageable: copies on the pool
+    host[:, :10] = 7
+    B.host_encode_batch(H.ReedSolomon(10, 4), host)
+    on_node = 0
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            if os.sched_getaffinity(int(tid)) == res["cpus"]:
+                on_node += 1
+        except OSError:
+            pass
+    assert on_node >= 15, (on_node, sorted(res["cpus"])[:8])

@@ -213,3 +213,21 @@ def test_file_errors_rebuilt_from_last_error_values():
         assert f"sys::HEC_ERR_{c} => EcShardError::{v}(a as usize, b as usize)" in body, v
     assert "c => EcShardError::ErasureCoding(to_err(c))" in body
     assert "unsafe { sys::hec_last_error_values(&mut a, &mut b, &mut e) }" in src
+
+
+def test_rust_sources_are_balanced():
+    """No compiler here: at least every brace, parenthesis and bracket of the
+    two crates balances (comments and string literals stripped)."""
+    for rel in (("rust", "helyim-ec-hip", "src", "lib.rs"), ("rust", "hec-sys", "src", "lib.rs")):
+        s = open(os.path.join(ROOT, *rel)).read()
+        s = re.sub(r"//[^\n]*", "", s)
+        s = re.sub(r'"(\\.|[^"\\])*"', '""', s)
+        depth = {"{": 0, "(": 0, "[": 0}
+        close = {"}": "{", ")": "(", "]": "["}
+        for ch in s:
+            if ch in depth:
+                depth[ch] += 1
+            elif ch in close:
+                depth[close[ch]] -= 1
+                assert depth[close[ch]] >= 0, (rel, ch)
+        assert all(v == 0 for v in depth.values()), (rel, depth)

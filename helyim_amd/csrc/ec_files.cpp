@@ -93,10 +93,26 @@ void io_error(ErrorSlot& e, const std::string& what) {
 // ---------------------------------------------------------------------------
 // Small fixed thread pool with fork/join task groups.
 // ---------------------------------------------------------------------------
+// Bind the file layer's I/O and writer threads to the device's NUMA node
+// (next to the pinned slots they fill and drain)? HEC_FILE_POOL_BIND=0 turns
+// it off (measurement only; tools/file_pool_bind_ab.sh).
+bool file_threads_bind() {
+    static const bool on = [] {
+        const char* v = std::getenv("HEC_FILE_POOL_BIND");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 class Pool {
    public:
-    explicit Pool(int n) {
-        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    // dev >= 0: workers bind themselves to that device's NUMA node.
+    Pool(int n, int dev) {
+        for (int i = 0; i < n; ++i)
+            th_.emplace_back([this, dev] {
+                if (dev >= 0) (void)hec_bind_thread_to_device(dev, nullptr);  // placement only
+                loop();
+            });
     }
     ~Pool() {
         {
@@ -242,7 +258,7 @@ struct StageClock {
 // small volumes do not pay for pinned allocation, streams and threads).
 class FilePipeline {
    public:
-    FilePipeline() : pool_(kIoThreads) {}
+    explicit FilePipeline(int dev) : pool_(kIoThreads, file_threads_bind() ? dev : -1), bind_dev_(dev) {}
     // Grow the slots to at least these sizes; call only while idle.
     int ensure(uint64_t host_bytes, uint64_t dev_bytes) {
         HEC_HIP(hipGetDevice(&dev_id_));
@@ -264,7 +280,11 @@ class FilePipeline {
         }
         host_cap_ = std::max(host_cap_, host_bytes);
         dev_cap_ = std::max(dev_cap_, dev_bytes);
-        if (!writer_.joinable()) writer_ = std::thread([this] { writer_loop(); });
+        if (!writer_.joinable())
+            writer_ = std::thread([this] {
+                if (file_threads_bind()) (void)hec_bind_thread_to_device(bind_dev_, nullptr);
+                writer_loop();
+            });
         return HEC_OK;
     }
     // Submit one job (blocks while its slot is still being written).
@@ -387,6 +407,7 @@ class FilePipeline {
     uint64_t host_cap_ = 0, dev_cap_ = 0;
     uint64_t next_ = 0;
     int dev_id_ = 0;
+    int bind_dev_ = 0;
     ErrorSlot err_;
     StageClock clk_;
 };
@@ -409,7 +430,7 @@ int lease_pipeline(uint64_t host_bytes, uint64_t dev_bytes, PipelineLease& out) 
     {
         std::lock_guard<std::mutex> lk(reg_mu);
         auto& slot = (*reg)[dev];
-        if (!slot.first) slot = {new std::mutex(), new FilePipeline()};
+        if (!slot.first) slot = {new std::mutex(), new FilePipeline(dev)};
         e = slot;
     }
     out.lock = std::unique_lock<std::mutex>(*e.first);  // one file operation per device at a time

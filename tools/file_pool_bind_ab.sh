@@ -7,9 +7,11 @@ set -e
 DIR=$(mktemp -d -p /dev/shm hec_ab.XXXX)
 trap 'rm -rf $DIR' EXIT
 python3 - "$DIR" <<'PY'
-import sys, numpy as np
-from oracle import rs_oracle as O
-open(sys.argv[1] + "/v.dat", "wb").write(O.splitmix64_bytes(99, 12 << 30).tobytes())
+import sys
+from oracle import corc
+with open(sys.argv[1] + "/v.dat", "wb") as f:
+    for g in range(12):  # 12 GiB, 1 GiB at a time
+        f.write(corc.splitmix64_bytes(99 + g, 1 << 30).tobytes())
 PY
 for round in 1 2 3; do
   for bind in 1 0; do

@@ -93,13 +93,16 @@ void io_error(ErrorSlot& e, const std::string& what) {
 // ---------------------------------------------------------------------------
 // Small fixed thread pool with fork/join task groups.
 // ---------------------------------------------------------------------------
-// Bind the file layer's I/O and writer threads to the device's NUMA node
-// (next to the pinned slots they fill and drain)? HEC_FILE_POOL_BIND=0 turns
-// it off (measurement only; tools/file_pool_bind_ab.sh).
+// Bind the file layer's I/O and writer threads to the device's NUMA node?
+// Off: measured on the GPU box (tools/file_pool_bind_ab.sh,
+// profiles/r04/file_pool_bind_ab.jsonl) a 12 GiB encode ran 25.3-28.6 GiB/s
+// bound against 28.9-30.1 unbound -- the .dat and shard pages in the page
+// cache sit on whichever node, and these threads touch them more than the
+// pinned slots. HEC_FILE_POOL_BIND=1 turns it on (measurement only).
 bool file_threads_bind() {
     static const bool on = [] {
         const char* v = std::getenv("HEC_FILE_POOL_BIND");
-        return !(v && v[0] == '0');
+        return v && v[0] == '1';
     }();
     return on;
 }

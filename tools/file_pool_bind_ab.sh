@@ -1,6 +1,6 @@
 # A/B of the file layer's thread placement (HEC_FILE_POOL_BIND=1: I/O and
-# writer threads bound to the GPU's NUMA node, the default; 0: inherited
-# affinity), alternating processes on one box over the same 12 GiB volume in
+# writer threads bound to the GPU's NUMA node; 0: inherited affinity, the
+# shipped default), alternating processes on one box over the same 12 GiB volume in
 # /dev/shm: write_ec_files 3x per process (fresh shard files each time) and a
 # 4-shard rebuild. One JSON line per process to stdout.
 set -e

@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kind", default="torch")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--precycle", action="store_true",
+                    help="allocate, touch and free a buffer of the batch's size first (torch kind)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -36,6 +38,12 @@ def main():
     shard = L + pad
     nbytes = S * 14 * shard
     raw = None
+    if args.precycle:
+        tmp = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        tmp.fill_(0)
+        torch.cuda.synchronize()
+        del tmp
+        torch.cuda.empty_cache()
     if args.kind == "torch":
         buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     else:
@@ -68,7 +76,7 @@ def main():
     enc = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     dec = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     alg = S * 14 * L
-    print(json.dumps({"kind": args.kind, "ptr": hex(t.data_ptr()), "enc_ms": round(enc, 4), "dec_ms": round(dec, 4),
+    print(json.dumps({"kind": args.kind, "precycle": args.precycle, "ptr": hex(t.data_ptr()), "enc_ms": round(enc, 4), "dec_ms": round(dec, 4),
                       "encode_frac": round(alg / enc / 1e6 / 8000, 4), "decode_frac": round(alg / dec / 1e6 / 8000, 4)}),
           flush=True)
     return 0

@@ -336,6 +336,7 @@ def e2e_section(rs, rank: int, S: int = 512, L: int = 1 << 20, reps: int = 3, de
     mem = ("pinned (hec_host_alloc: this GPU's NUMA node)" if devices is None else
            "pinned (hec_host_alloc_multi: each range on its GPU's NUMA node)")
     return {"stripes": S, "shard_len": L, "host_memory": mem,
+            "encode_kernel": H.lib.hec_host_encode_kernel_name(L).decode(),
             "host_numa_node": node, "devices": devices if devices is not None else "current",
             "raw": {"data_bytes": data * reps, "encode": [enc0, enc1], "decode": [dec0, dec1]},
             "encode_data_GiB_s": round(data / te / 2**30, 2),

@@ -393,7 +393,7 @@ int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s) {
 int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uint64_t in_stripe,
               uint64_t in_shard, uint8_t* out_base, uint64_t out_stripe, uint64_t out_shard,
               uint64_t len, uint32_t n_stripes, const uint32_t* masks, uint32_t* bad,
-              hipStream_t s, Completion* done) {
+              hipStream_t s, Completion* done, bool over_pcie) {
     ApplyArgs a{};
     if (done) HEC_TRY(done->arm(s, &a.done_count, &a.done_flag, &a.done_seq));
     a.in_base = in_base;
@@ -416,8 +416,23 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
     const uint64_t align = uint64_t(reinterpret_cast<uintptr_t>(in_base)) | in_stripe | in_shard |
                            uint64_t(reinterpret_cast<uintptr_t>(out_base)) | out_stripe | out_shard;
     const bool aligned = (align % 16) == 0;
-    HEC_HIP(launch_apply(a, int(nin), aligned, launch_config(), s));
+    const LaunchConfig cfg = over_pcie && !masks ? pcie_encode_config(launch_config()) : launch_config();
+    HEC_HIP(launch_apply(a, int(nin), aligned, cfg, s));
     return HEC_OK;
+}
+
+// Over PCIe the encode's bytes arrive at the link's rate, so its VALU cost is
+// free and the narrower column range per workgroup wins: the 8 B-per-lane
+// table encode ran 50.5-52.9 GiB/s of data against 49.4-51.1 for the
+// bit-sliced kernel on 512 x 1 MiB pinned stripes, alternating in one process
+// on two boxes, ahead in each of the 7 rounds (tools/e2e_encode_kernel_probe.py, profiles/r04/e2e_encode_kernels_*.jsonl).
+LaunchConfig pcie_encode_config(const LaunchConfig& cfg) {
+    LaunchConfig c = cfg;
+    if (c.pcie_enc_narrow && c.mode == 0) {
+        c.bitslice = 0;
+        c.enc_vec_bytes = 8;
+    }
+    return c;
 }
 
 // ---------------------------------------------------------------------------
@@ -793,6 +808,15 @@ int hec_set_encode_kernel(int kind) {
     if (kind != 0 && kind != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0 or 1");
     update_launch_config([&](LaunchConfig& c) { c.bitslice = kind; });
     return HEC_OK;
+}
+
+int hec_set_host_encode_narrow(int on) {
+    update_launch_config([&](LaunchConfig& c) { c.pcie_enc_narrow = on ? 1 : 0; });
+    return HEC_OK;
+}
+
+const char* hec_host_encode_kernel_name(uint64_t shard_len) {
+    return encode_kernel_name(shard_len, pcie_encode_config(launch_config()));
 }
 
 int hec_set_ragged_encode_remap(int on) {

@@ -291,9 +291,13 @@ void parallel_for(size_t n, uint64_t bytes, F fn) {
 
 // Run one plan set over a strided batch (plan 0 for every stripe unless masks).
 // done (optional): the launch signals it (Completion::arm) when it finishes.
+// over_pcie: an encode whose buffers are host memory (zero copy).
 int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uint64_t in_stripe,
               uint64_t in_shard, uint8_t* out_base, uint64_t out_stripe, uint64_t out_shard,
               uint64_t len, uint32_t n_stripes, const uint32_t* masks, uint32_t* bad,
-              hipStream_t s, Completion* done = nullptr);
+              hipStream_t s, Completion* done = nullptr, bool over_pcie = false);
+// The launch configuration a zero-copy host-batch encode (kernel streaming
+// host memory over PCIe) runs under: the knobs, with pcie_enc_narrow applied.
+LaunchConfig pcie_encode_config(const LaunchConfig& cfg);
 
 }  // namespace hec

@@ -292,7 +292,7 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
         if ((rc = p->reserve(0, 1))) return rc;
         if ((rc = run_apply(gd->encode, uint32_t(k), zd, data_stripe_stride, data_shard_stride, zp,
                             parity_stripe_stride, parity_shard_stride, shard_len, n_stripes, nullptr, nullptr,
-                            p->streams[0])))
+                            p->streams[0], nullptr, /*over_pcie=*/true)))
             return rc;
         HEC_HIP(hipStreamSynchronize(p->streams[0]));
         return HEC_OK;
@@ -328,7 +328,8 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
                                 h_data + (s0 + s) * data_stripe_stride + i * data_shard_stride, shard_len);
                 });
                 if ((rc = run_apply(gd->encode, uint32_t(k), zs[q], dstripe, Lp, zs[q] + uint64_t(k) * Lp, dstripe,
-                                    Lp, (shard_len + 15) / 16 * 16, c, nullptr, nullptr, st)))
+                                    Lp, (shard_len + 15) / 16 * 16, c, nullptr, nullptr, st, nullptr,
+                                    /*over_pcie=*/true)))
                     return rc;
                 HEC_HIP(hipEventRecord(p->hdone[q], st));
                 if (it > 0) {  // chunk it-1 (other slot) is done or nearly: hand its parity back

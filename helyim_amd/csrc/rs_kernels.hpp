@@ -120,6 +120,10 @@ struct LaunchConfig {
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
                                  // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
                                  // multiply (speed only)
+    int pcie_enc_narrow = 1;     // zero-copy host-batch encodes (the kernel streams host memory over
+                                 // PCIe): 1 = the 8-byte-per-lane table encode where the shard length
+                                 // is a multiple of 2 KiB (default; 3.5% faster over PCIe than the
+                                 // bit-sliced kernel), 0 = the device batches' choice (speed only)
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees

@@ -451,6 +451,15 @@ int hec_set_host_staging(uint64_t max_bytes);
 /* Host batches on pinned memory: 1 = zero-copy kernels (default), 0 = the
  * copy pipeline. Speed only; identical results. Returns HEC_OK. */
 int hec_set_host_zero_copy(int on);
+/* Zero-copy host-batch encodes (the kernel streams host memory over PCIe;
+ * hec_host_encode_batch[_multi] on pinned memory and the pageable path's
+ * pinned slots): 1 = the 8-byte-per-lane table encode where the shard length
+ * is a multiple of 2 KiB (default: ~3.5% faster over PCIe than the bit-sliced
+ * kernel), 0 = the device batches' kernel. Speed only. Returns HEC_OK. */
+int hec_set_host_encode_narrow(int on);
+/* Name of the kernel a zero-copy host-batch encode of this shard length runs
+ * under the current knobs (static string). */
+const char* hec_host_encode_kernel_name(uint64_t shard_len);
 /* Diagnostic: *zero_copy = 1 when [p, p + bytes) is one pinned range the
  * current device can address, i.e. host batches on it are coded zero-copy
  * (hec_host_alloc, hec_host_alloc_multi, hipHostMalloc, torch pin_memory),

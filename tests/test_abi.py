@@ -363,3 +363,25 @@ def test_every_failure_resets_the_detail_and_values(tmp_path):
     with pytest.raises(H.TooFewShardsPresent):
         rs.reconstruct_batch([[np.zeros(8, np.uint8)] * 14, [None] * 5 + [np.zeros(8, np.uint8)] * 9])
     assert _lib.last_detail() == "stripe 1"
+
+
+def test_host_encode_kernel_over_pcie():
+    """Zero-copy host-batch encodes (the kernel streams host memory over PCIe)
+    take the 8-byte-per-lane table encode where the shard length is a
+    multiple of 2 KiB (hec_set_host_encode_narrow, default on); device
+    batches keep the bit-sliced kernel; off = the device batches' choice."""
+    import helyim_amd as H
+    lib = H.lib
+    L = 1 << 20
+    try:
+        assert lib.hec_host_encode_kernel_name(L).decode().startswith("rs104_narrow_kernel<DEC=false, 8 B per lane>")
+        assert lib.hec_encode_kernel_name(L).decode().startswith("rs104_bs_encode_kernel")
+        assert lib.hec_host_encode_kernel_name(4096 + 16).decode().startswith("rs104_kernel<DEC=false>")
+        assert lib.hec_set_host_encode_narrow(0) == 0
+        assert lib.hec_host_encode_kernel_name(L).decode() == lib.hec_encode_kernel_name(L).decode()
+        assert lib.hec_set_host_encode_narrow(1) == 0
+        assert lib.hec_set_kernel_mode(1) == 0  # the XOR-only diagnostic is never swapped for the narrow kernel
+        assert lib.hec_host_encode_kernel_name(L).decode() == lib.hec_encode_kernel_name(L).decode()
+    finally:
+        lib.hec_set_host_encode_narrow(1)
+        lib.hec_set_kernel_mode(0)

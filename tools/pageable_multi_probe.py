@@ -4,8 +4,10 @@ one host worker pool, so all but one copied their staging serially; round 4
 gives each device up to two pools). One GPU: the PCIe link is shared, so this
 measures the host-side copy parallelism, not more bandwidth.
 
-usage: python tools/pageable_multi_probe.py [--stripes 512] [--reps 3] [--rounds 3]
-prints one JSON line per (round, device list)."""
+usage: python tools/pageable_multi_probe.py [--stripes 512] [--reps 3] [--rounds 3] [--single]
+prints one JSON line per (round, device list); --single: the one-call row
+only. The line names the library it loaded (HEC_LIB_PATH selects another
+build, for alternating-process A/Bs on one box)."""
 import argparse
 import json
 import os
@@ -22,6 +24,7 @@ def main():
     ap.add_argument("--shard-len", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--single", action="store_true")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -33,7 +36,8 @@ def main():
     t = torch.zeros((S, 14, L), dtype=torch.uint8)  # pageable
     t[:, :10] = torch.randint(0, 256, (S, 10, L), dtype=torch.uint8)
     masks = np.full(S, 0x3FFF & ~0b1001000010001, np.uint32)
-    lists = {"single": None, "[0,0]": [0, 0], "[0,0,0,0]": [0, 0, 0, 0]}
+    lists = {"single": None} if args.single else {"single": None, "[0,0]": [0, 0], "[0,0,0,0]": [0, 0, 0, 0]}
+    lib_name = os.path.relpath(H._lib.LIB_PATH, ROOT)
     for name, devs in lists.items():  # warm-up: pipelines, pools, tables
         B.host_encode_batch(rs, t, devices=devs)
         B.host_reconstruct_batch(rs, t, masks, devices=devs)
@@ -47,10 +51,10 @@ def main():
             for _ in range(args.reps):
                 B.host_reconstruct_batch(rs, t, masks, devices=devs)
             t2 = time.perf_counter()
-            print(json.dumps({"round": r, "devices": name, "memory": "pageable", "stripes": S, "shard_len": L,
+            print(json.dumps({"lib": lib_name, "round": r, "devices": name, "memory": "pageable",
+                              "stripes": S, "shard_len": L,
                               "encode_data_GiB_s": round(data * args.reps / (t1 - t0) / 2**30, 2),
                               "decode_data_GiB_s": round(data * args.reps / (t2 - t1) / 2**30, 2)}), flush=True)
-
 
 if __name__ == "__main__":
     main()

@@ -1,12 +1,16 @@
 """Stage timing of the GPU file layer (write_ec_files / rebuild_ec_files) on a
 synthetic volume in /dev/shm: run with HEC_FILE_TRACE=1 to get the pipeline's
-per-stage seconds on stderr. Measurement only.
+per-stage seconds on stderr. Each call also reports the process's CPU
+seconds (user + system, all threads) beside its wall time, and the cgroup's
+CPU quota: CPU-seconds near quota x wall means the call is CPU-bound.
+Measurement only.
 
 python tools/file_stages.py [--gib 12] [--reps 2]
 """
 import argparse
 import json
 import os
+import resource
 import shutil
 import sys
 import tempfile
@@ -14,6 +18,21 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def cpu_s():
+    """user + system CPU seconds of this process, all threads"""
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_utime + r.ru_stime
+
+
+def cpu_quota():
+    """the cgroup's CPU limit (cpu.max: quota / period), or None"""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -30,21 +49,24 @@ def main():
         base = os.path.join(d, "v")
         nbytes = int(args.gib * 2**30)
         make_volume(base + ".dat", nbytes)
-        out = {"dir": args.dir, "dat_bytes": nbytes, "fresh": args.fresh, "encode_s": [], "rebuild_s": []}
+        out = {"dir": args.dir, "dat_bytes": nbytes, "fresh": args.fresh, "encode_s": [], "rebuild_s": [],
+               "encode_cpu_s": [], "rebuild_cpu_s": [], "cpu_quota": cpu_quota()}
         H.write_ec_files(base)  # warm-up: device tables, pinned staging
         for _ in range(args.reps):
             if args.fresh:
                 for i in range(14):
                     os.remove(base + H.to_ext(i))
-            t0 = time.perf_counter()
+            c0, t0 = cpu_s(), time.perf_counter()
             H.write_ec_files(base)
             out["encode_s"].append(round(time.perf_counter() - t0, 4))
+            out["encode_cpu_s"].append(round(cpu_s() - c0, 3))
         for _ in range(args.reps):
             for i in (0, 5, 10, 13):
                 os.remove(base + H.to_ext(i))
-            t0 = time.perf_counter()
+            c0, t0 = cpu_s(), time.perf_counter()
             H.rebuild_ec_files(base)
             out["rebuild_s"].append(round(time.perf_counter() - t0, 4))
+            out["rebuild_cpu_s"].append(round(cpu_s() - c0, 3))
         out["encode_GiB_s"] = round(args.gib / min(out["encode_s"]), 3)
         out["rebuild_GiB_s"] = round(args.gib / min(out["rebuild_s"]), 3)
         print(json.dumps(out), flush=True)

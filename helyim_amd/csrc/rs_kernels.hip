@@ -1041,11 +1041,15 @@ static const char* rs104_name(const Rs104Pick& p, bool dec, bool xo) {
     }
 }
 
+constexpr const char* kNoLaunch = "none (empty shards: EmptyShard, no launch)";
+
 const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
+    if (len == 0) return kNoLaunch;
     return rs104_name(rs104_pick(len, 1, true, cfg), true, cfg.mode == 1);
 }
 
 const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
+    if (len == 0) return kNoLaunch;
     return rs104_name(rs104_pick(len, 1, false, cfg), false, cfg.mode == 1);
 }
 

@@ -480,7 +480,9 @@ int hec_set_completion_signal(uint64_t max_bytes);
 /* Version string of the library build. */
 const char* hec_version(void);
 /* Name of the kernel a 16-byte-aligned RS(10,4) device batch encode of this
- * shard length runs under the current launch configuration (static string). */
+ * shard length runs under the current launch configuration (static string;
+ * shard_len 0, which fails with HEC_ERR_EMPTY_SHARD before any launch, names
+ * no kernel: "none (...)"). */
 const char* hec_encode_kernel_name(uint64_t shard_len);
 /* Same for a 16-byte-aligned in-place RS(10,4) device batch reconstruct. */
 const char* hec_decode_kernel_name(uint64_t shard_len);

@@ -377,6 +377,8 @@ def test_host_encode_kernel_over_pcie():
         assert lib.hec_host_encode_kernel_name(L).decode().startswith("rs104_narrow_kernel<DEC=false, 8 B per lane>")
         assert lib.hec_encode_kernel_name(L).decode().startswith("rs104_bs_encode_kernel")
         assert lib.hec_host_encode_kernel_name(4096 + 16).decode().startswith("rs104_kernel<DEC=false>")
+        for name in (lib.hec_host_encode_kernel_name(0), lib.hec_encode_kernel_name(0), lib.hec_decode_kernel_name(0)):
+            assert name.decode().startswith("none")  # empty shards never launch
         assert lib.hec_set_host_encode_narrow(0) == 0
         assert lib.hec_host_encode_kernel_name(L).decode() == lib.hec_encode_kernel_name(L).decode()
         assert lib.hec_set_host_encode_narrow(1) == 0

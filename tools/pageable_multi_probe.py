@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--single", action="store_true")
+    ap.add_argument("--alternate", default="", help="env var libhec reads per call (e.g. HEC_STREAM_COPY): "
+                    "each case runs with it =1 and =0, alternating in this process")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -42,8 +44,12 @@ def main():
         B.host_encode_batch(rs, t, devices=devs)
         B.host_reconstruct_batch(rs, t, masks, devices=devs)
     data = S * 10 * L
+    settings = ["1", "0"] if args.alternate else [None]
+    cases = [(name, devs, v) for name, devs in lists.items() for v in settings]
     for r in range(args.rounds):
-        for name, devs in lists.items():
+        for name, devs, v in cases:
+            if v is not None:
+                os.environ[args.alternate] = v
             t0 = time.perf_counter()
             for _ in range(args.reps):
                 B.host_encode_batch(rs, t, devices=devs)
@@ -51,10 +57,12 @@ def main():
             for _ in range(args.reps):
                 B.host_reconstruct_batch(rs, t, masks, devices=devs)
             t2 = time.perf_counter()
-            print(json.dumps({"lib": lib_name, "round": r, "devices": name, "memory": "pageable",
+            tag = {args.alternate: v} if v is not None else {}
+            print(json.dumps({"lib": lib_name, **tag, "round": r, "devices": name, "memory": "pageable",
                               "stripes": S, "shard_len": L,
                               "encode_data_GiB_s": round(data * args.reps / (t1 - t0) / 2**30, 2),
                               "decode_data_GiB_s": round(data * args.reps / (t2 - t1) / 2**30, 2)}), flush=True)
+
 
 if __name__ == "__main__":
     main()

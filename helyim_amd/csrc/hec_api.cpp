@@ -621,6 +621,7 @@ static int encode_host(const hec_rs* rs, const uint8_t* const* data, uint8_t* co
                      [&](size_t j) { std::memcpy(dst_of(int(j)), hpar + j * Lp, L); });
         return HEC_OK;
     }
+    const StreamDrain drain{sc->stream};  // the D2H copies below write caller memory
     for (int i = 0; i < rs->k; ++i)
         HEC_HIP(hipMemcpyAsync(sc->dbuf + i * Lp, data[i], L, hipMemcpyHostToDevice, sc->stream));
     if ((rc = run_apply(gd->encode, uint32_t(rs->k), sc->dbuf, 0, Lp, par, 0, Lp, round_up(L, 16), 1,
@@ -668,6 +669,7 @@ static int reconstruct_host(const hec_rs* rs, uint8_t* const* shards, const size
     HostPlans hp;
     hp.add(coefs, in_ids, out_ids);
     if ((rc = sc->adhoc.upload(hp, nullptr, sc->stream))) return rc;
+    const StreamDrain drain{sc->stream};  // the D2H copies below write caller memory
     for (uint32_t id : in_ids)
         HEC_HIP(hipMemcpyAsync(sc->dbuf + id * Lp, shards[id], L, hipMemcpyHostToDevice, sc->stream));
     if ((rc = run_apply(sc->adhoc, uint32_t(rs->k), sc->dbuf, 0, Lp, sc->dbuf, 0, Lp, round_up(L, 16), 1,

@@ -182,6 +182,17 @@ struct ScratchTrim {
         if (on) sc->trim_large();
     }
 };
+// Drains a stream when its scope ends, whatever the return path. For calls
+// that queue copies or kernels onto CALLER memory: an error return between
+// two enqueues must not leave that work in flight once the caller, told the
+// call failed, frees or reuses its buffers. Success paths have synchronised
+// already, so the drain finds the stream idle.
+struct StreamDrain {
+    hipStream_t s;
+    ~StreamDrain() {
+        if (s && hipStreamSynchronize(s) != hipSuccess) (void)hipGetLastError();
+    }
+};
 // Scratch slots per device: a host call leases one (its own stream, staging
 // buffers and completion flag), so concurrent calls from several threads
 // overlap on the GPU instead of queueing behind one mutex (SURVEY.md §8b:

@@ -52,9 +52,7 @@ struct Pipeline {
     // Free the large staging (the pageable path's pinned slots and the copy
     // path's device slots); streams, events and mask words stay. The next
     // call on this pipeline reserves again.
-    void trim() {
-        for (auto& st : streams)  // (calls end synchronised; this is belt and braces)
-            if (st) (void)hipStreamSynchronize(st);
+    void trim() {  // (the lease has drained the streams)
         for (auto& h : hslot) {
             if (h) (void)hipHostFree(h);
             h = nullptr;
@@ -127,8 +125,15 @@ struct PipelineLease {
     Lease<Pipeline> lease;
     bool trim_after = false;
     Pipeline* operator->() const { return lease.sc; }
-    ~PipelineLease() {
-        if (trim_after && lease.sc) lease.sc->trim();  // still holding the pipeline's mutex
+    ~PipelineLease() {  // still holding the pipeline's mutex
+        if (!lease.sc) return;
+        // Host batches code caller memory in place (zero copy) or copy into
+        // it: an error return between enqueues must not leave that work in
+        // flight for the caller's freed buffers (StreamDrain's rule). After
+        // a successful call every stream is idle already.
+        for (auto st : lease.sc->streams)
+            if (st && hipStreamSynchronize(st) != hipSuccess) (void)hipGetLastError();
+        if (trim_after) lease.sc->trim();
     }
 };
 

@@ -20,8 +20,9 @@
  * Threading: a hec_rs_t is immutable after hec_rs_new and may be shared by
  * threads (upstream ReedSolomon is Send + Sync). Device state (tables,
  * decode-pattern cache, staging buffers) is per device and mutex guarded.
- * Host-memory entry points synchronise before returning; the hec_gpu_*
- * batch entry points are asynchronous on the caller's stream.
+ * Host-memory entry points synchronise before returning, on error returns
+ * too (no copy or kernel touching caller memory is left in flight); the
+ * hec_gpu_* batch entry points are asynchronous on the caller's stream.
  */
 #ifndef HEC_H
 #define HEC_H

@@ -5,6 +5,7 @@
 // chunk i+1, the kernel of chunk i and the D2H copy of chunk i-1 overlap
 // (PCIe Gen5 x16 is full duplex; the copy engines run beside the kernel).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -195,6 +196,15 @@ uint64_t batch_span(uint64_t stripe_stride, uint64_t shard_stride, uint32_t shar
     return uint64_t(stripes - 1) * stripe_stride + uint64_t(shards - 1) * shard_stride + len;
 }
 
+// Test hook: HEC_TEST_HOST_FAIL_AFTER_CHUNK=i fails a copy-pipeline encode
+// right after queueing chunk i's kernel, so a test can check that the work
+// queued before an error return has landed when the call returns
+// (tests/test_gpu_host_batch.py). Read per call; -1 = off.
+int forced_failure_chunk() {
+    const char* v = std::getenv("HEC_TEST_HOST_FAIL_AFTER_CHUNK");
+    return v && *v ? std::atoi(v) : -1;
+}
+
 uint32_t chunk_stripes(uint64_t shard_len, int n, uint32_t n_stripes) {
     uint64_t c = std::max<uint64_t>(1, kChunkBytes / (uint64_t(n) * shard_len));
     return uint32_t(std::min<uint64_t>(c, n_stripes));
@@ -350,6 +360,7 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
         }
     }
     if ((rc = p->reserve(size_t(C) * rs->n * Lp, 1))) return rc;
+    const int fail_at = forced_failure_chunk();
     for (uint32_t s0 = 0, it = 0; s0 < n_stripes; s0 += C, ++it) {
         const uint32_t c = std::min(C, n_stripes - s0);
         const int q = int(it % kDepth);
@@ -362,6 +373,7 @@ int hec_host_encode_batch(const hec_rs_t* rs, const uint8_t* h_data, uint64_t da
         if ((rc = run_apply(gd->encode, uint32_t(k), d, dstripe, Lp, d + uint64_t(k) * Lp, dstripe, Lp,
                             (shard_len + 15) / 16 * 16, c, nullptr, nullptr, st)))
             return rc;
+        if (int(it) == fail_at) return fail(HEC_ERR_HIP, "test hook: failure after chunk " + std::to_string(it));
         for (uint32_t s = 0; s < c; ++s)
             HEC_HIP(copy2d(h_parity + (s0 + s) * parity_stripe_stride, parity_shard_stride,
                            d + s * dstripe + uint64_t(k) * Lp, Lp, shard_len, uint64_t(m), hipMemcpyDeviceToHost, st));

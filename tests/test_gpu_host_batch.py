@@ -388,3 +388,30 @@ def test_host_encode_kernel_choice_over_pcie(gpu, L, narrow):
         assert np.array_equal(u.numpy()[:, 10:], a[:, 10:])
     finally:
         lib.hec_set_host_encode_narrow(1)
+
+
+def test_error_return_leaves_nothing_in_flight(gpu, monkeypatch):
+    """A host batch that fails part-way returns only once the work it had
+    queued onto the caller's buffers has landed (hec.h: nothing in flight on
+    error returns). HEC_TEST_HOST_FAIL_AFTER_CHUNK=2 fails a copy-pipeline
+    encode right after queueing chunk 2's kernel: at return, chunks 0-1 hold
+    the oracle's parity, and chunk 2's (never copied back) and later chunks'
+    parity rows are untouched. A 1 MiB stripe is 14 MiB, so a 96 MiB chunk
+    holds 6 stripes (host_pipeline.cpp kChunkBytes)."""
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    assert H.lib.hec_set_host_zero_copy(0) == 0  # the copy pipeline (reset by the host_path fixture)
+    rs = H.ReedSolomon(10, 4)
+    S, L, C = 24, 1 << 20, 6
+    t = _host_stripes(S, L, pin=False)
+    a = t.numpy()
+    a[:, 10:] = 0xA5
+    ref = corc.encode_stripes(np.ascontiguousarray(a[:, :10]))
+    monkeypatch.setenv("HEC_TEST_HOST_FAIL_AFTER_CHUNK", "2")
+    with pytest.raises(H.DeviceError, match="test hook: failure after chunk 2"):
+        B.host_encode_batch(rs, t)
+    assert np.array_equal(a[:2 * C, 10:], ref[:2 * C])
+    assert (a[2 * C:, 10:] == 0xA5).all()
+    monkeypatch.delenv("HEC_TEST_HOST_FAIL_AFTER_CHUNK")
+    B.host_encode_batch(rs, t)  # the pipeline is usable again
+    assert np.array_equal(a[:, 10:], ref)

@@ -260,7 +260,7 @@ int hec_rs_reconstruct_batch(const hec_rs_t* rs, uint8_t* const* shards, const s
             else if (np && li != L) err = HEC_ERR_INCORRECT_SHARD_SIZE;
             L = li;
             ++np;
-            mask |= 1u << i;
+            if (i < 32) mask |= 1u << i;  // used by the RS(10,4) path only; n may be up to 256
         }
         if (!err && np < n && np < k) err = HEC_ERR_TOO_FEW_SHARDS_PRESENT;
         if (!err && np < n)

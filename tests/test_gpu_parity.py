@@ -60,6 +60,49 @@ def test_generic_geometry_encode_reconstruct(gpu, k, m):
                 assert np.array_equal(got[i], ref[i]), (k, m, L, sorted(erased), i)
 
 
+@pytest.mark.parametrize("k,m", [(255, 1), (1, 255), (128, 128), (200, 56)])
+def test_widest_geometries_encode_reconstruct(gpu, k, m):
+    """The widest codecs upstream accepts (data + parity = 256, the GF(2^8)
+    limit; ReedSolomon::new refuses 257) through the per-call API: encode,
+    verify, and reconstruct / reconstruct_data with the most erasures the code
+    can take (m), the first m data shards erased, and every parity shard
+    erased, against the numpy oracle."""
+    import helyim_amd as H
+    rng = np.random.default_rng(4000 + 7 * k + m)
+    n = k + m
+    rs, ors = H.ReedSolomon(k, m), O.ReedSolomon(k, m)
+    with pytest.raises(H.TooManyShards):
+        H.ReedSolomon(k, m + 1)
+    for L in (1, 4096 + 3):
+        data = [_rand(rng, L) for _ in range(k)]
+        sh = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+        ref = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+        rs.encode(sh)
+        ors.encode(ref)
+        for i in range(n):
+            assert np.array_equal(sh[i], ref[i]), (k, m, L, i)
+        assert rs.verify(sh)
+        patterns = [set(rng.choice(n, m, replace=False).tolist()), set(range(min(k, m))), set(range(k, n))]
+        for erased in patterns:
+            got = [None if i in erased else ref[i].copy() for i in range(n)]
+            rs.reconstruct(got)
+            for i in range(n):
+                assert np.array_equal(got[i], ref[i]), (k, m, L, i)
+            got = [None if i in erased else ref[i].copy() for i in range(n)]
+            rs.reconstruct_data(got)
+            for i in range(n):
+                if i in erased and i >= k:
+                    assert got[i] is None
+                else:
+                    assert np.array_equal(got[i], ref[i]), (k, m, L, i)
+        # the batched degraded-read entry point, one stripe per pattern
+        stripes = [[None if i in erased else ref[i].copy() for i in range(n)] for erased in patterns]
+        rs.reconstruct_batch(stripes)
+        for st in stripes:
+            for i in range(n):
+                assert np.array_equal(st[i], ref[i]), (k, m, L, i)
+
+
 def test_reconstruct_host_api_patterns(gpu):
     import helyim_amd as H
     rng = np.random.default_rng(7)

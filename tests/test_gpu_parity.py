@@ -103,6 +103,41 @@ def test_widest_geometries_encode_reconstruct(gpu, k, m):
                 assert np.array_equal(st[i], ref[i]), (k, m, L, i)
 
 
+@pytest.mark.parametrize("k,m", [(255, 1), (128, 128), (1, 255)])
+def test_widest_geometries_batch_encode(gpu, k, m):
+    """Batch encodes of the widest codecs (the plan kernel with up to 255
+    inputs or outputs): a device batch and a pinned and a pageable host batch
+    (zero copy and the copy pipeline), against the C oracle. (Batch
+    reconstructs take per-stripe masks and stop at 16 shards.)"""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    rng = np.random.default_rng(5000 + k)
+    n, S, L = k + m, 3, 4096 + 5
+    rs, ors = H.ReedSolomon(k, m), corc.CReedSolomon(k, m)
+    host = np.zeros((S, n, L), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    for s in range(S):
+        ors.encode([host[s, i] for i in range(n)])
+    t = torch.zeros((S, n, L), dtype=torch.uint8, device="cuda")
+    t[:, :k] = torch.from_numpy(host[:, :k]).cuda()
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), host)
+    for pin in (True, False):
+        for zc in (1, 0):
+            assert H.lib.hec_set_host_zero_copy(zc) == 0
+            try:
+                h = torch.zeros((S, n, L), dtype=torch.uint8)
+                if pin:
+                    h = h.pin_memory()
+                h.numpy()[:, :k] = host[:, :k]
+                B.host_encode_batch(rs, h)
+                assert np.array_equal(h.numpy(), host), (pin, zc)
+            finally:
+                H.lib.hec_set_host_zero_copy(1)
+
+
 def test_reconstruct_host_api_patterns(gpu):
     import helyim_amd as H
     rng = np.random.default_rng(7)

@@ -7,7 +7,7 @@ SRC := $(wildcard helyim_amd/csrc/*.cpp) $(wildcard helyim_amd/csrc/*.hip)
 HDR := $(wildcard helyim_amd/csrc/*.hpp) $(wildcard helyim_amd/csrc/*.inc) include/hec.h
 OBJ := $(patsubst helyim_amd/csrc/%,build/obj/%.o,$(SRC))
 
-all: helyim_amd/libhec.so oracle build/cabi_bench
+all: helyim_amd/libhec.so oracle build/cabi_bench build/membench_calib
 
 helyim_amd/libhec.so: $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -lpthread
@@ -27,6 +27,13 @@ oracle:
 build/cabi_bench: tools/cabi_bench.cpp include/hec.h helyim_amd/libhec.so
 	@mkdir -p build
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lhelyim_amd -lhec -Wl,-rpath,'$$ORIGIN/../helyim_amd'
+
+# FETCH_SIZE / WRITE_SIZE calibration streams + the shipped kernels in one
+# process (tools/membench.hip calib; profiles/pmc_traffic.json "calibration").
+build/membench_calib: tools/membench.hip include/hec.h helyim_amd/libhec.so
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -DMEMBENCH_WITH_HEC -o $@ $< -Lhelyim_amd -lhec \
+	    -Wl,-rpath,'$$ORIGIN/../helyim_amd'
 
 # Measurement variants of the kernel file (cache policy of shard streams).
 VARIANTS := ntl0_nts0 ntl0_nts1 ntl1_nts0 null lf0 s_sc1 s_sc0sc1 s_sc0sc1nt s_bufnt l_bufnt

@@ -276,6 +276,38 @@ def cpu_baseline_threads(seconds: float = 5.0, threads: int = 16) -> dict:
                                       f"stripe per thread, {el:.1f} s"}
 
 
+def cpu_baseline_legs(seconds: float, allowed, stand_in: bool = False) -> dict:
+    """The CPU path timed on this box's host cores, in the same run as the GPU
+    legs, at ANY world size (north_star: "next to helyim-ec's CPU path timed
+    on the GPU box's own host cores in the same run"). Rank 0 runs it after
+    the last GPU barrier while the other ranks wait at the closing barrier.
+
+    cpu_baseline: 1 thread. cpu_baseline_threads: 16 threads (the box's CPU
+    share per GPU). cpu_baseline_cores: one thread per CPU this process can
+    actually run on at once: min(physical cores, affinity mask, cgroup quota);
+    "quota_bound" says the quota (or affinity), not the core count, set it.
+    stand_in: the same record shapes without running anything (--dry-run)."""
+    os.sched_setaffinity(0, allowed)  # the CPU legs get every CPU this process may use
+    cores = physical_cores()
+    usable = cores["affinity_cpus"]
+    if cores["cgroup_cpu_quota"]:
+        usable = min(usable, max(1, int(cores["cgroup_cpu_quota"])))
+    n_cores = max(1, min(cores["physical_cores"], usable))
+    bound = {"quota_bound": cores["physical_cores"] > usable,
+             "threads_note": "one thread per usable CPU: min(physical cores, affinity, cgroup quota)"}
+    if stand_in:
+        rec = {"value": 0.0, "unit": "GiB/s", "kind": "stand_in", "sample": "dry run: nothing timed"}
+        return {"cpu_baseline": dict(rec, cores=1), "cpu_baseline_threads": dict(rec, cores=16),
+                "cpu_baseline_cores": dict(rec, cores=n_cores, **cores, **bound)}
+    out = {"cpu_baseline": cpu_baseline(seconds),
+           "cpu_baseline_threads": cpu_baseline_threads(seconds / 2, 16)}
+    if n_cores == 16:  # the same measurement as the 16-thread leg: not run twice
+        out["cpu_baseline_cores"] = dict(out["cpu_baseline_threads"], **cores, **bound)
+    else:
+        out["cpu_baseline_cores"] = dict(cpu_baseline_threads(seconds / 2, n_cores), **cores, **bound)
+    return out
+
+
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -601,6 +633,9 @@ def parse_args(argv=None):
     ap.add_argument("--shard-len", type=int, default=1 << 20)
     ap.add_argument("--shard-pad", type=int, default=64 << 10,
                     help="HBM layout: shard stride = shard_len + this (DESIGN.md 'Data layout in HBM')")
+    ap.add_argument("--base-align", type=int, default=0,
+                    help="start the batch at a multiple of this many bytes inside an over-allocation "
+                         "(power of two; 0 = the allocator's base; measurement, VERDICT r04 item 1(c))")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the end-to-end and mixed-workload sections")
@@ -701,6 +736,8 @@ def dry_run(args, world: int, rank: int, local_rank: int) -> int:
                "ms_per_step": round(t_job / args.steps * 1e3, 4), "scaling": "weak", "verified": chk_ok,
                "rank_seed_bases": [r["seed_base"] for r in per_rank], "ranks": per_rank}
         out.update(extras)
+        if not args.no_cpu_baseline:
+            out.update(cpu_baseline_legs(args.cpu_seconds, os.sched_getaffinity(0), stand_in=True))
         print(json.dumps(out), flush=True)
     return 0 if chk_ok else 3
 
@@ -725,7 +762,8 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
 
     S, L = args.stripes, args.shard_len
     rs = H.ReedSolomon(K_DATA, M_PARITY)
-    t = B.empty_stripes(S, N_TOTAL, L, shard_pad=args.shard_pad)
+    t = B.empty_stripes(S, N_TOTAL, L, shard_pad=args.shard_pad, base_align=args.base_align)
+    base_alignment = B.address_alignment(t.data_ptr())
     B.fill_stripes_splitmix(t, K_DATA, rank_seed_base(rank))  # same bytes as a packed batch
     masks = torch.from_numpy(erasure_masks(S, rank)).cuda()
     stream = torch.cuda.current_stream()
@@ -772,10 +810,13 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
     B.reconstruct_batch(rs, t, masks)
     torch.cuda.synchronize()
     del er
-    bad = corc.check_device_batch(t, masks.cpu().numpy(),
-                                  data_seeds=rank_seed_base(rank) + np.arange(S, dtype=np.uint64))
+    # the seeded-data check regenerates splitmix64 words, so it needs whole
+    # 8-byte words per shard; other lengths check parity and rebuilt shards only
+    seeds = rank_seed_base(rank) + np.arange(S, dtype=np.uint64) if L % 8 == 0 else None
+    bad = corc.check_device_batch(t, masks.cpu().numpy(), data_seeds=seeds)
     chk_ok = not bad
     verification = {"stripes_checked": S, "rebuilt_shards_checked": 4 * S, "mismatched_stripes": bad[:16],
+                    "data_seeds_checked": seeds is not None,
                     "seconds": round(time.perf_counter() - v0, 2),
                     "method": "erased shards zeroed and rebuilt, every stripe vs the C oracle (seeded data, "
                               "encode, reconstruct from survivors), 16 threads"}
@@ -861,6 +902,7 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
                                    f"(BASELINE configs 2+3), device-resident",
                        "stripes_per_gpu": S, "shard_len": L, "erasures_per_stripe": 4,
                        "shard_stride": t_shard_stride,
+                       "base_alignment": base_alignment,
                        "parallelism": f"independent stripe batches x{world}"},
             # the dominant kernel: the launch with the larger share of the step
             "roofline": dominant,
@@ -883,13 +925,8 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
             "ranks": per_rank,
         }
         out.update(extras)
-        if world == 1 and not args.no_cpu_baseline:
-            os.sched_setaffinity(0, allowed)  # the CPU baseline gets every CPU this process may use
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-            cores = physical_cores()
-            out["cpu_baseline_threads"] = cpu_baseline_threads(args.cpu_seconds / 2, 16)
-            out["cpu_baseline_cores"] = dict(cpu_baseline_threads(args.cpu_seconds / 2, cores["physical_cores"]),
-                                             **cores)
+        if not args.no_cpu_baseline:  # every world size; the other ranks wait at main()'s closing barrier
+            out.update(cpu_baseline_legs(args.cpu_seconds, allowed))
         print(json.dumps(out), flush=True)
     return 0 if chk_ok else 3
 

@@ -605,8 +605,15 @@ int hec_host_staging_stats(int* n_pipelines, uint64_t* pinned_bytes, uint64_t* d
     int n = 0;
     uint64_t pinned = 0, devb = 0;
     if (pool) {
-        std::lock_guard<std::mutex> g(pool->mu);
-        for (auto& sl : pool->slots) {
+        // Slots are never removed from a pool, so their addresses stay valid;
+        // the pool mutex is held only to copy them, never while waiting on a
+        // slot (that would stall every lease on the device behind one call).
+        std::vector<Pipeline*> slots;
+        {
+            std::lock_guard<std::mutex> g(pool->mu);
+            for (auto& sl : pool->slots) slots.push_back(sl.get());
+        }
+        for (Pipeline* sl : slots) {
             std::lock_guard<std::mutex> l(sl->mu);  // waits for a call in flight on it
             ++n;
             pinned += sl->pinned_bytes();

@@ -162,7 +162,13 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     if ((rc = sc->reserve(total, meta))) return rc;
     if ((rc = ensure_dense_decode(rs, gd, sc->stream))) return rc;
     // survivors the decode reads (the first k present shards) -> slots 0..k-1
-    std::atomic<int> first_err{HEC_OK};
+    // The fills may run on host-pool workers, whose failure detail and values
+    // are thread-local to them: the first failure's (code, detail, values) is
+    // captured on its thread and re-raised on the caller's.
+    std::mutex err_mu;
+    int first_err = HEC_OK;
+    std::string err_detail;
+    ErrorValues err_values;
     // one task per (job, slot): a single large interval's 10 survivor reads run
     // in parallel too
     auto fill_one = [&](size_t t) {
@@ -174,8 +180,12 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
                 if (used == want) {
                     const int r = fill(j, used, i, sc->host + lay[j].off + used * lay[j].Lp);
                     if (r) {
-                        int expect = HEC_OK;
-                        first_err.compare_exchange_strong(expect, r);
+                        std::lock_guard<std::mutex> g(err_mu);
+                        if (first_err == HEC_OK) {
+                            first_err = r;
+                            err_detail = hec_last_error_detail();
+                            err_values = last_error_values();
+                        }
                     }
                     return;
                 }
@@ -186,7 +196,7 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
         parallel_io_for(jobs.size() * size_t(k), in_total, fill_one);
     else
         parallel_for(jobs.size() * size_t(k), in_total, fill_one);
-    if (first_err.load()) return first_err.load();
+    if (first_err) return fail_with(first_err, err_detail, err_values);
     // zero-copy: the kernel reads the packed survivors and writes the rebuilt
     // shards in the pinned staging itself (no H2D / D2H of the payload)
     uint8_t* zh = zero_copy_enabled() ? pinned_device_ptr(sc->host) : nullptr;

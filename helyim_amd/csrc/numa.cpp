@@ -204,7 +204,7 @@ int hec_bind_thread_to_device(int device, int* n_cpus) {
     cpu_set_t allowed, want;
     CPU_ZERO(&want);
     if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0)
-        return fail(HEC_ERR_IO, std::string("sched_getaffinity: ") + strerror(errno));
+        return fail_errno(HEC_ERR_IO, "sched_getaffinity", errno);
     int n = 0;
     for (int c : cpus)
         if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) {
@@ -213,7 +213,7 @@ int hec_bind_thread_to_device(int device, int* n_cpus) {
         }
     if (n == 0) return HEC_OK;  // none of the node's CPUs is ours (container cpuset): leave as is
     if (sched_setaffinity(0, sizeof(want), &want) != 0)
-        return fail(HEC_ERR_IO, std::string("sched_setaffinity: ") + strerror(errno));
+        return fail_errno(HEC_ERR_IO, "sched_setaffinity", errno);
     if (n_cpus) *n_cpus = n;
     return HEC_OK;
 }
@@ -312,8 +312,8 @@ int hec_host_numa_node(const void* p, int* node) {
     int status = -1;
     // move_pages with nodes == NULL only reports where each page lives
     if (syscall(SYS_move_pages, 0, 1ul, &page, nullptr, &status, 0) != 0)
-        return fail(HEC_ERR_IO, std::string("move_pages: ") + strerror(errno));
-    if (status < 0) return fail(HEC_ERR_IO, std::string("page not resident: ") + strerror(-status));
+        return fail_errno(HEC_ERR_IO, "move_pages", errno);
+    if (status < 0) return fail_errno(HEC_ERR_IO, "page not resident", -status);
     *node = status;
     return HEC_OK;
 }

@@ -123,6 +123,40 @@ def test_eight_rank_dry_run_assembles_the_node_line():
     assert len(mixed["per_rank"]) == 8
     window = (max(m["raw"]["e2e"][1] for m in mixed["per_rank"]) - min(m["raw"]["e2e"][0] for m in mixed["per_rank"]))
     assert mixed["aggregate_end_to_end_data_GiB_s"] == pytest.approx(sum(range(1, 9)) / window, rel=0.02)
+    # VERDICT r04 "next" 2: the CPU path is in the line at every world size,
+    # through the same function run_rank uses (bench.cpu_baseline_legs)
+    for key, threads in (("cpu_baseline", 1), ("cpu_baseline_threads", 16)):
+        assert out[key]["kind"] == "stand_in" and out[key]["cores"] == threads
+    cores = out["cpu_baseline_cores"]
+    assert {"physical_cores", "affinity_cpus", "cgroup_cpu_quota", "quota_bound"} <= set(cores)
+    usable = min(cores["affinity_cpus"], int(cores["cgroup_cpu_quota"] or cores["affinity_cpus"]))
+    assert cores["cores"] == max(1, min(cores["physical_cores"], usable))
+    assert cores["quota_bound"] == (cores["physical_cores"] > usable)
+
+
+def test_cpu_baseline_cores_sized_to_the_quota(monkeypatch):
+    """cpu_baseline_cores runs one thread per CPU the process can use at once:
+    under a 16-CPU cgroup quota on a 128-core host that is 16 threads, marked
+    quota_bound (round 4 ran 128 threads under the quota and reported a
+    throttled figure as a core-count result)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setattr(bench, "physical_cores", lambda: {"physical_cores": 128, "logical_cpus": 256,
+                                                          "affinity_cpus": 256, "cgroup_cpu_quota": 16.0})
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: None)
+    runs = []
+    monkeypatch.setattr(bench, "cpu_baseline", lambda s: {"value": 1.0, "cores": 1})
+    monkeypatch.setattr(bench, "cpu_baseline_threads",
+                        lambda s, n: runs.append(n) or {"value": float(n), "cores": n})
+    out = bench.cpu_baseline_legs(1.0, set())
+    assert out["cpu_baseline_cores"]["cores"] == 16 and out["cpu_baseline_cores"]["quota_bound"] is True
+    assert runs == [16]  # the 16-thread leg is not run twice
+    monkeypatch.setattr(bench, "physical_cores", lambda: {"physical_cores": 8, "logical_cpus": 16,
+                                                          "affinity_cpus": 16, "cgroup_cpu_quota": None})
+    runs.clear()
+    out = bench.cpu_baseline_legs(1.0, set())
+    assert runs == [16, 8] and out["cpu_baseline_cores"]["cores"] == 8
+    assert out["cpu_baseline_cores"]["quota_bound"] is False
 
 
 def test_dry_run_one_failing_rank_fails_the_job():

@@ -390,20 +390,24 @@ def test_host_encode_kernel_choice_over_pcie(gpu, L, narrow):
         lib.hec_set_host_encode_narrow(1)
 
 
-def test_error_return_leaves_nothing_in_flight(gpu, monkeypatch):
+@pytest.mark.parametrize("pin", [True, False])
+def test_error_return_leaves_nothing_in_flight(gpu, monkeypatch, pin):
     """A host batch that fails part-way returns only once the work it had
     queued onto the caller's buffers has landed (hec.h: nothing in flight on
     error returns). HEC_TEST_HOST_FAIL_AFTER_CHUNK=2 fails a copy-pipeline
     encode right after queueing chunk 2's kernel: at return, chunks 0-1 hold
     the oracle's parity, and chunk 2's (never copied back) and later chunks'
     parity rows are untouched. A 1 MiB stripe is 14 MiB, so a 96 MiB chunk
-    holds 6 stripes (host_pipeline.cpp kChunkBytes)."""
+    holds 6 stripes (host_pipeline.cpp kChunkBytes). The pinned case is the
+    one that exercises the drain: its device-to-host copies land in the
+    caller's buffer asynchronously (a pageable destination is staged by the
+    runtime and lands before the copy call returns)."""
     import helyim_amd as H
     import helyim_amd.batch as B
     assert H.lib.hec_set_host_zero_copy(0) == 0  # the copy pipeline (reset by the host_path fixture)
     rs = H.ReedSolomon(10, 4)
     S, L, C = 24, 1 << 20, 6
-    t = _host_stripes(S, L, pin=False)
+    t = _host_stripes(S, L, pin=pin)
     a = t.numpy()
     a[:, 10:] = 0xA5
     ref = corc.encode_stripes(np.ascontiguousarray(a[:, :10]))

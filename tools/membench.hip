@@ -8,7 +8,8 @@
 //               (10R4W == the encode pattern with the math removed)
 // One workgroup (256 lanes x 16 B) per 4 KiB chunk unless noted.
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/membench tools/membench.hip
-// Run:   build/membench [pad|mix]  (prints one JSON line per case)
+// Run:   build/membench [pad|mix|calib]  (prints one JSON line per case)
+// calib: make build/membench_calib (links libhec; see calib() below)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -128,6 +129,46 @@ __global__ __launch_bounds__(256) void k_10r4w_pol(uint8_t* base, uint64_t strip
     }
 }
 
+// FETCH_SIZE / WRITE_SIZE calibration: the decode's own
+// access pattern with the math removed, over a KNOWN byte count. VB bytes per
+// lane (8 = global_load_dwordx2 like rs104_narrow_kernel, 16 = dwordx4), one
+// workgroup per 256 * VB byte column range of one stripe, XCD eighths remap,
+// reads shards 0..9 non-temporal, then either writes shards 10..13 (W = 4,
+// the decode's 4-erasure pattern) or nothing (W = 0: read-only).
+template <int VB>
+struct VecOf;
+template <>
+struct VecOf<8> {
+    typedef uint32_t T __attribute__((ext_vector_type(2)));
+};
+template <>
+struct VecOf<16> {
+    typedef uint32_t T __attribute__((ext_vector_type(4)));
+};
+template <int VB, int W>
+__global__ __launch_bounds__(256) void k_cal(uint8_t* base, uint64_t stripe_stride, uint64_t shard_stride,
+                                            uint32_t chunks_per_stripe, uint32_t* sink) {
+    typedef typename VecOf<VB>::T V;
+    const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blockIdx.x % 8;
+    const uint32_t b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
+    const uint32_t stripe = b / chunks_per_stripe, chunk = b % chunks_per_stripe;
+    uint8_t* s = base + uint64_t(stripe) * stripe_stride;
+    const uint64_t o = uint64_t(chunk) * (256 * VB) + threadIdx.x * VB;
+    V d[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) d[i] = __builtin_nontemporal_load(reinterpret_cast<const V*>(s + i * shard_stride + o));
+    V acc = d[0];
+#pragma unroll
+    for (int i = 1; i < 10; ++i) acc ^= d[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        V w = acc;
+        w.x ^= j;
+        __builtin_nontemporal_store(w, reinterpret_cast<V*>(s + (10 + j) * shard_stride + o));
+    }
+    if (W == 0 && acc.x == 0x12345678u && acc.y == 0x9abcdef0u) sink[threadIdx.x] = acc.x;  // practically never
+}
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b)); }
@@ -205,7 +246,73 @@ static int mix_sweep() {
     return 0;
 }
 
+// libhec's own batch entry points, for the calibration pass: the decode and
+// encode run in the SAME rocprofv3 PMC pass as the calibration streams
+// (build: make build/membench_calib, linked against helyim_amd/libhec.so).
+#ifdef MEMBENCH_WITH_HEC
+#include "../include/hec.h"
+#endif
+
+// Calibration pass: known-byte streams at 8 and 16 B per lane, then the
+// shipped RS(10,4) encode and 4-erasure decode on the same padded batch
+// (shard stride 1 MiB + 64 KiB, as bench.py). Each case runs `reps` times;
+// tools/pmc_summary.py divides the known bytes by the counters.
+static int calib() {
+    const uint64_t S = 4096, L = 1ull << 20, N = 14, ss = L + 65536;
+    const int reps = 3;
+    uint8_t* buf;
+    CHECK(hipMalloc(&buf, S * N * ss));
+    CHECK(hipMemset(buf, 0x5a, S * N * ss));
+    uint32_t* sink;
+    CHECK(hipMalloc(&sink, 4096));
+    char extra[160];
+#define CAL(VB, W)                                                                                          \
+    {                                                                                                       \
+        const uint32_t cps = uint32_t(L / (256 * VB));                                                      \
+        snprintf(extra, sizeof extra, ", \"bytes_per_lane\": %d, \"read_bytes\": %llu, \"write_bytes\": %llu", \
+                 VB, (unsigned long long)(S * 10 * L), (unsigned long long)(S * W * L));                     \
+        run("cal_" #VB "B_10r" #W "w", extra, double(S * (10 + W) * L), [&] {                               \
+            hipLaunchKernelGGL((k_cal<VB, W>), dim3(uint32_t(S * cps)), dim3(256), 0, 0, buf, N * ss, ss, cps, sink); \
+        }, reps);                                                                                           \
+    }
+    CAL(8, 0); CAL(8, 4); CAL(16, 0); CAL(16, 4);
+#undef CAL
+#ifdef MEMBENCH_WITH_HEC
+    hec_rs_t* rs = nullptr;
+    if (hec_rs_new(10, 4, &rs)) { fprintf(stderr, "hec_rs_new failed\n"); return 1; }
+    std::vector<uint32_t> masks(S);
+    uint64_t z = 0x9E3779B97F4A7C15ull;
+    for (uint64_t s = 0; s < S; ++s) {  // 4 distinct erasures per stripe
+        uint32_t m = (1u << 14) - 1;
+        while (__builtin_popcount(m) > 10) {
+            z ^= z << 13, z ^= z >> 7, z ^= z << 17;
+            m &= ~(1u << (z % 14));
+        }
+        masks[s] = m;
+    }
+    uint32_t* dmask;
+    CHECK(hipMalloc(&dmask, S * 4));
+    CHECK(hipMemcpy(dmask, masks.data(), S * 4, hipMemcpyHostToDevice));
+    snprintf(extra, sizeof extra, ", \"algorithmic_bytes\": %llu, \"kernel\": \"%s\"", (unsigned long long)(S * 14 * L),
+             hec_encode_kernel_name(L));
+    run("hec_encode", extra, double(S * 14 * L), [&] {
+        if (hec_gpu_encode_batch(rs, buf, N * ss, ss, buf + 10 * ss, N * ss, ss, L, uint32_t(S), nullptr)) exit(1);
+    }, reps);
+    snprintf(extra, sizeof extra, ", \"algorithmic_bytes\": %llu, \"kernel\": \"%s\"", (unsigned long long)(S * 14 * L),
+             hec_decode_kernel_name(L));
+    run("hec_decode", extra, double(S * 14 * L), [&] {
+        if (hec_gpu_reconstruct_batch(rs, buf, N * ss, ss, L, uint32_t(S), dmask, nullptr, nullptr)) exit(1);
+    }, reps);
+    CHECK(hipFree(dmask));
+    hec_rs_free(rs);
+#endif
+    CHECK(hipFree(sink));
+    CHECK(hipFree(buf));
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "calib") return calib();
     if (argc > 1 && std::string(argv[1]) == "pad") return pad_sweep();
     if (argc > 1 && std::string(argv[1]) == "mix") return mix_sweep();
     const uint64_t S = 4096, L = 1ull << 20, N = 14;

@@ -1,6 +1,7 @@
-"""Per process of tools/tlb_probe.sh: the bench line's encode / decode
-fractions beside the UTCL1 translation counters per full-size dispatch.
-usage: python tools/tlb_summary.py gpurun_out/tlb K"""
+"""Per process of tools/align_probe.sh: the bench line's encode / decode
+fractions and batch base alignment beside the UTCL1 translation counters per
+full-size dispatch (the process's arm from arm_<i>.txt).
+usage: python tools/tlb_summary.py gpurun_out/align [K]"""
 import csv
 import json
 import os
@@ -9,7 +10,8 @@ import sys
 
 
 def main():
-    d, k = sys.argv[1], int(sys.argv[2])
+    d = sys.argv[1]
+    k = int(sys.argv[2]) if len(sys.argv) > 2 else len([x for x in os.listdir(d) if x.startswith("bench_")])
     for i in range(1, k + 1):
         line = [x for x in open(os.path.join(d, f"bench_{i}.log"), errors="replace") if x.startswith('{"metric"')]
         b = json.loads(line[-1]) if line else {}
@@ -23,7 +25,10 @@ def main():
                 continue  # full-size dispatches only
             kind = "decode" if "narrow" in r["Kernel_Name"] else "encode"
             per.setdefault((kind, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
-        out = {"proc": i, "encode_frac": b.get("encode", {}).get("frac"), "decode_frac": b.get("decode", {}).get("frac")}
+        arm_f = os.path.join(d, f"arm_{i}.txt")
+        out = {"proc": i, "arm": open(arm_f).read().strip() if os.path.exists(arm_f) else None,
+               "base_alignment": b.get("config", {}).get("base_alignment"),
+               "encode_frac": b.get("encode", {}).get("frac"), "decode_frac": b.get("decode", {}).get("frac")}
         for (kind, name), v in sorted(per.items()):
             out[f"{kind}.{name.replace('TCP_UTCL1_', '').replace('_sum', '')}"] = statistics.median(v)
         print(json.dumps(out))

@@ -288,6 +288,19 @@ int hec_write_ec_files(const char* base_filename);
  * exercise the large-row path). */
 int hec_write_ec_files_ex(const char* base_filename, uint64_t buf_size, uint64_t large_block_size,
                           uint64_t small_block_size);
+/* File-level coding path (speed only; the shard bytes are the same): 1 =
+ * zero copy through the page cache (default): the .dat and the shard files
+ * the GPU writes are mmap'd and registered with the GPU, the kernels read and
+ * write the file pages over PCIe, the data shards of an encode are written
+ * from the .dat mapping; 0 = the staged pipeline (pread into pinned staging,
+ * H2D, kernel, D2H, pwritev). Where the runtime refuses to register file
+ * pages the zero-copy call falls back to the staged pipeline by itself.
+ * Process-wide; takes effect at the next call. */
+int hec_set_file_zero_copy(int on);
+/* Process totals of file-level calls (write_ec_files / rebuild_ec_files with
+ * rows to code) that ran zero copy, and of those that fell back to the staged
+ * pipeline because the runtime or the files refused the mapping. */
+int hec_file_path_stats(uint64_t* zero_copy_calls, uint64_t* fallbacks);
 /* rebuild_ec_files(base_filename) -> Vec<u32> (encoder.rs:48-50, 73-109,
  * 244-307): recreates every missing .ecNN. rebuilt_ids (capacity 14) receives
  * the rebuilt shard ids in ascending order, *n_rebuilt their count. */

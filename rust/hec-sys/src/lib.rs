@@ -199,6 +199,8 @@ extern "C" {
     pub fn hec_set_host_staging(max_bytes: u64) -> c_int;
     pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;
     pub fn hec_set_host_zero_copy(on: c_int) -> c_int;
+    pub fn hec_set_file_zero_copy(on: c_int) -> c_int;
+    pub fn hec_file_path_stats(zero_copy_calls: *mut u64, fallbacks: *mut u64) -> c_int;
     pub fn hec_set_host_encode_narrow(on: c_int) -> c_int;
     pub fn hec_host_encode_kernel_name(shard_len: u64) -> *const c_char;
     pub fn hec_host_zero_copy_view(p: *const c_void, bytes: u64, zero_copy: *mut c_int) -> c_int;

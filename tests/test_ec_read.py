@@ -401,3 +401,35 @@ def test_ec_volume_degraded_reads_concurrent(gpu, tmp_path):
         for x in th:
             x.join()
     assert not errors
+
+
+@pytest.mark.gpu
+def test_degraded_read_worker_error_reaches_the_caller(gpu, tmp_path):
+    """a survivor read that fails inside the batched
+    degraded read runs on a host-pool worker once the interval's 10 survivor
+    reads total >= 256 KiB (parallel_io_for); its detail and values must come
+    back on the caller's thread, not the caller's stale ones. A 600 KB needle
+    in shard 0's block is lost (shard 0 dropped); after mounting, survivor
+    shard 5 is truncated, so its read returns short: Io "shard shrank", errno
+    0 -- and not the "is not found" Io the same thread raised just before."""
+    import helyim_amd as H
+    size = 600_000
+    body = 16 + size + 4
+    actual = body + (8 - body % 8)
+    base = str(tmp_path / "big")
+    dat = O.splitmix64_bytes(77, 8 + actual + 64).tobytes()
+    open(base + ".dat", "wb").write(dat)
+    H.write_ec_files(base)
+    open(base + ".idx", "wb").write(struct.pack(">QIi", 7, 1, size))
+    O.write_sorted_file_from_index(base)
+    _drop(base, [0])
+    with H.EcVolume(base) as v:
+        assert v.read_needle(7) == _needle_bytes(dat, 1, size)  # degraded read, intact survivors
+        with open(base + O.to_ext(5), "r+b") as f:
+            f.truncate(0)
+        with pytest.raises(H.Io, match="is not found"):
+            v.read_needle(123456789)  # leaves a stale Io detail on this thread
+        with pytest.raises(H.Io) as ei:
+            v.read_needle(7)
+    assert "shrank" in ei.value.detail and O.to_ext(5) in ei.value.detail, ei.value.detail
+    assert ei.value.errno == 0 and ei.value.os_error is None

@@ -14,7 +14,34 @@ def _sha(path):
     return O.sha256(open(path, "rb").read())
 
 
-def test_volume_30mb_encode_rebuild(gpu, golden, tmp_path):
+def _path_stats():
+    import ctypes
+    import helyim_amd as H
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    assert H.lib.hec_file_path_stats(ctypes.byref(a), ctypes.byref(b)) == 0
+    return a.value, b.value
+
+
+@pytest.fixture(params=["zero_copy", "staged"])
+def file_path(request):
+    """Both file-level coding paths (hec_set_file_zero_copy): zero copy
+    through the page cache (default) and the staged pipeline. Under
+    zero_copy, every call that coded rows must really have run zero copy:
+    the fallback counter may not move."""
+    import helyim_amd as H
+    assert H.lib.hec_set_file_zero_copy(1 if request.param == "zero_copy" else 0) == 0
+    before = _path_stats()
+    yield request.param
+    after = _path_stats()
+    H.lib.hec_set_file_zero_copy(1)
+    if request.param == "zero_copy":
+        assert after[1] == before[1], "a file call fell back to the staged pipeline"
+        assert after[0] > before[0], "no file call ran zero copy"
+    else:
+        assert after == before
+
+
+def test_volume_30mb_encode_rebuild(gpu, golden, tmp_path, file_path):
     import helyim_amd as H
     g = golden("volume_30mb.json")
     base = str(tmp_path / "1")
@@ -31,7 +58,7 @@ def test_volume_30mb_encode_rebuild(gpu, golden, tmp_path):
 
 
 @pytest.mark.parametrize("size", [1, 639, 640, 641, 2000, 6401, 6400 * 2 + 3, 6400 * 3])
-def test_small_geometry_vs_oracle(gpu, tmp_path, size):
+def test_small_geometry_vs_oracle(gpu, tmp_path, size, file_path):
     """Large-row path exercised with 640-byte 'large' and 32-byte 'small' blocks."""
     import helyim_amd as H
     buf, large, small = 16, 640, 32
@@ -91,7 +118,7 @@ def test_rebuild_errors(gpu, tmp_path):
     assert _sha(base + H.to_ext(3)) == shas[3]
 
 
-def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path):
+def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path, file_path):
     """Shard files smaller than 1 MiB (row = file size), mirrored by the oracle."""
     import helyim_amd as H
     rs = O.ReedSolomon(10, 4)
@@ -109,7 +136,7 @@ def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path):
         assert open(base + H.to_ext(i), "rb").read() == sh[i].tobytes()
 
 
-def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path):
+def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path, file_path):
     """hec_set_device per thread (hec.h): volumes encoded and rebuilt
     concurrently from several threads, round-robin over the visible devices
     (all on device 0 on a one-GPU box), each byte-identical to the fixture."""
@@ -150,7 +177,7 @@ def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path):
         assert [_sha(b + H.to_ext(i)) for i in range(14)] == g["shard_sha256"]
 
 
-def test_randomised_file_geometry_vs_oracle(gpu, tmp_path):
+def test_randomised_file_geometry_vs_oracle(gpu, tmp_path, file_path):
     """Seeded sweep of generate_ec_files over block geometries (buffer,
     large and small block sizes) and .dat sizes around the large-row rule
     (large rows only while remaining > 10 large blocks, encoder.rs:215),
@@ -190,7 +217,7 @@ def _file_digest(path):
     return h.hexdigest()
 
 
-def test_production_geometry_multi_slice_multi_job_vs_oracle(gpu, tmp_path):
+def test_production_geometry_multi_slice_multi_job_vs_oracle(gpu, tmp_path, file_path):
     """The file-layer paths a real 30,000 MB volume takes, at a size the C
     oracle finishes in seconds: 48 MiB large blocks (three 16 MiB slices per
     large block, ec_files.cpp kLargeSlice), 1 MiB small blocks, 256 KiB
@@ -247,7 +274,7 @@ def _same_file(a, b, chunk=1 << 28):
 
 
 @pytest.mark.parametrize("extra", [0, 4097])
-def test_reference_geometry_large_row_threshold(gpu, extra):
+def test_reference_geometry_large_row_threshold(gpu, extra, file_path):
     """The reference's own constants (1 GiB large blocks, 1 MiB small blocks,
     256 KiB buffers) at the large-row threshold, encoder.rs:215 (`remaining >
     large_block_size * DATA_SHARDS_COUNT`, strict): a .dat of exactly 10 GiB

@@ -95,8 +95,8 @@ void io_error(ErrorSlot& e, const std::string& what) {
 // Small fixed thread pool with fork/join task groups.
 // ---------------------------------------------------------------------------
 // Bind the file layer's I/O and writer threads to the device's NUMA node?
-// Off: measured on the GPU box (tools/file_pool_bind_ab.sh,
-// profiles/r04/file_pool_bind_ab.jsonl) a 12 GiB encode ran 25.3-28.6 GiB/s
+// Off: measured on the GPU box (profiles/r04/file_pool_bind_ab.jsonl,
+// profiles/r04/INDEX.md) a 12 GiB encode ran 25.3-28.6 GiB/s
 // bound against 28.9-30.1 unbound -- the .dat and shard pages in the page
 // cache sit on whichever node, and these threads touch them more than the
 // pinned slots. HEC_FILE_POOL_BIND=1 turns it on (measurement only).
@@ -460,7 +460,7 @@ struct Rs104 {
 // shards on the box's overlay filesystem: 0.16 s with, 0.54-0.78 s without).
 // Skipped on tmpfs, where fallocate zero-fills the page cache up front and
 // the writes then copy over it (12 GiB volume in /dev/shm: 0.37-0.40 s fresh
-// without, 0.47-0.65 s with; tools/ab_prealloc*.sh). Filesystems without
+// without, 0.47-0.65 s with; profiles/r01/ab_prealloc.txt). Filesystems without
 // fallocate are skipped silently. HEC_NO_PREALLOC=1 turns it off (measurement).
 std::shared_future<void> preallocate_async(const int* fds, int n, uint64_t bytes) {
     static const bool disabled = std::getenv("HEC_NO_PREALLOC") != nullptr;

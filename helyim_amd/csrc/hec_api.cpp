@@ -428,7 +428,7 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
 // free and the narrower column range per workgroup wins: the 8 B-per-lane
 // table encode ran 50.5-52.9 GiB/s of data against 49.4-51.1 for the
 // bit-sliced kernel on 512 x 1 MiB pinned stripes, alternating in one process
-// on two boxes, ahead in each of the 7 rounds (tools/e2e_encode_kernel_probe.py, profiles/r04/e2e_encode_kernels_*.jsonl).
+// on two boxes, ahead in each of the 7 rounds (profiles/r04/e2e_encode_kernels_*.jsonl, profiles/r04/INDEX.md).
 LaunchConfig pcie_encode_config(const LaunchConfig& cfg) {
     LaunchConfig c = cfg;
     if (c.pcie_enc_narrow && c.mode == 0) {

@@ -136,7 +136,7 @@ int current_device(int* dev);
 // Completion of one small host call without hipStreamSynchronize: the
 // launch's last workgroup stores a sequence number into a pinned host flag
 // (signal_done in rs_kernels.hip) and the caller spins on it. Measured on
-// MI355X (tools/latency_probe.hip): a one-workgroup zero-copy stripe
+// MI355X (profiles/r02/latency_completion_signal.jsonl): a one-workgroup zero-copy stripe
 // completes in 9.2 us this way against 13.3 us through hipStreamSynchronize.
 // Owned by a scratch object, so calls on it are serialised by its mutex.
 struct Completion {

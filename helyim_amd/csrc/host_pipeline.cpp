@@ -167,7 +167,7 @@ hipError_t copy2d(void* dst, uint64_t dpitch, const void* src, uint64_t spitch, 
 // (hipHostMalloc / torch pin_memory) is handed to the kernel as is, so the
 // kernel's loads and stores cross PCIe themselves -- no staging slots, no SDMA
 // copies, both directions at once. Measured 51 GiB/s of data encoded vs 41-44
-// for the copy pipeline (tools/zerocopy_probe.hip). The whole
+// for the copy pipeline (profiles/r02/HISTORY.md "host path"). The whole
 // [p, p + span) must be one registered host range; anything else (pageable
 // memory, device memory, a range running past the allocation) takes the copy
 // pipeline. hec_set_host_zero_copy(0) disables it (measurement).

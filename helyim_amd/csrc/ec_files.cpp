@@ -512,8 +512,7 @@ void add_reads(std::vector<ReadSeg>& v, int fd, uint64_t host_off, uint64_t len,
 }
 
 // ---------------------------------------------------------------------------
-// Zero copy through the page cache (the default where the GPU can register
-// file pages; hec_set_file_zero_copy).
+// Zero copy through the page cache (opt-in: hec_set_file_zero_copy(1)).
 // ---------------------------------------------------------------------------
 // The staged pipeline above copies every byte twice on the CPU: pread of the
 // .dat into pinned staging, pwritev of all 14 shards out of it (a 12 GiB
@@ -527,8 +526,14 @@ void add_reads(std::vector<ReadSeg>& v, int fd, uint64_t host_off, uint64_t len,
 // an encode are byte copies of .dat blocks: the CPU pwritev()s them straight
 // out of the .dat mapping while the GPU codes. Left on the CPU: one copy of
 // the data and the zeroing of fresh output pages.
+// Measured and NOT the default (profiles/r05/file_stages_b.json, a 12 GiB
+// volume in /dev/shm, alternating calls): zero copy 2.30-2.43 s encode /
+// 1.28-1.71 s rebuild against 0.51-0.54 / 0.33-0.40 s staged, on 16.3-17.3
+// against 7.0-7.7 CPU-seconds. Registering 4 KiB page-cache pages costs more
+// than copying them: populate + register 0.73-1.14 s and unregister 0.46-0.49 s
+// per 16.8 GiB, against ~0.45 s for the staged pipeline's whole pread.
 std::atomic<int>& file_zero_copy_mode() {
-    static std::atomic<int> m{1};
+    static std::atomic<int> m{0};
     return m;
 }
 constexpr int kFallback = -1000;  // internal status: registration refused, take the staged path

@@ -288,14 +288,16 @@ int hec_write_ec_files(const char* base_filename);
  * exercise the large-row path). */
 int hec_write_ec_files_ex(const char* base_filename, uint64_t buf_size, uint64_t large_block_size,
                           uint64_t small_block_size);
-/* File-level coding path (speed only; the shard bytes are the same): 1 =
- * zero copy through the page cache (default): the .dat and the shard files
- * the GPU writes are mmap'd and registered with the GPU, the kernels read and
- * write the file pages over PCIe, the data shards of an encode are written
- * from the .dat mapping; 0 = the staged pipeline (pread into pinned staging,
- * H2D, kernel, D2H, pwritev). Where the runtime refuses to register file
- * pages the zero-copy call falls back to the staged pipeline by itself.
- * Process-wide; takes effect at the next call. */
+/* File-level coding path (speed only; the shard bytes are the same): 0 =
+ * the staged pipeline (default: pread into pinned staging, H2D, kernel, D2H,
+ * pwritev); 1 = zero copy through the page cache: the .dat and the shard
+ * files the GPU writes are mmap'd and registered with the GPU, the kernels
+ * read and write the file pages over PCIe, the data shards of an encode are
+ * written from the .dat mapping. Zero copy measured 4x slower on a 12 GiB
+ * page-cached volume (registering 4 KiB pages costs more than copying them;
+ * DESIGN.md §5). Where the runtime or the files refuse the mapping, a
+ * zero-copy call falls back to the staged pipeline by itself. Process-wide;
+ * takes effect at the next call. */
 int hec_set_file_zero_copy(int on);
 /* Process totals of file-level calls (write_ec_files / rebuild_ec_files with
  * rows to code) that ran zero copy, and of those that fell back to the staged

@@ -24,8 +24,8 @@ def _path_stats():
 
 @pytest.fixture(params=["zero_copy", "staged"])
 def file_path(request):
-    """Both file-level coding paths (hec_set_file_zero_copy): zero copy
-    through the page cache (default) and the staged pipeline. Under
+    """Both file-level coding paths (hec_set_file_zero_copy): the staged
+    pipeline (default) and zero copy through the page cache. Under
     zero_copy, every call that coded rows must really have run zero copy:
     the fallback counter may not move."""
     import helyim_amd as H
@@ -33,7 +33,7 @@ def file_path(request):
     before = _path_stats()
     yield request.param
     after = _path_stats()
-    H.lib.hec_set_file_zero_copy(1)
+    H.lib.hec_set_file_zero_copy(0)
     if request.param == "zero_copy":
         assert after[1] == before[1], "a file call fell back to the staged pipeline"
         assert after[0] > before[0], "no file call ran zero copy"

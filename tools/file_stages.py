@@ -78,7 +78,7 @@ def main():
                 H.rebuild_ec_files(base)
                 r["rebuild_s"].append(round(time.perf_counter() - t0, 4))
                 r["rebuild_cpu_s"].append(round(cpu_s() - c0, 3))
-        H.lib.hec_set_file_zero_copy(1)
+        H.lib.hec_set_file_zero_copy(0)  # the default
         for p in paths:
             r = out["paths"][p]
             r["encode_GiB_s"] = round(args.gib / min(r["encode_s"]), 3)

@@ -328,18 +328,12 @@ uint64_t ragged_chunks(const hec_stripe_desc& d, bool decode, uint32_t chunk_byt
 // and hec_ragged_kernel_name so a reported name is the kernel that runs.
 struct RaggedPick {
     bool bitslice;  // encode with every length a multiple of 8 KiB: rs104_bs_ragged_kernel
-    bool narrow;    // decode with every length a multiple of 2 KiB: rs104_ragged_narrow_kernel
     bool remap;     // XCD eighths (else dispatch order)
-    uint32_t chunk_bytes() const { return bitslice ? kBsChunk : narrow ? kNarrowChunk : 4096; }
 };
 RaggedPick ragged_pick(const hec_stripe_desc* descs, uint32_t n, bool decode, const LaunchConfig& cfg) {
     RaggedPick p;
     p.bitslice = !decode && cfg.bitslice != 0 && cfg.mode == 0;
     for (uint32_t j = 0; j < n && p.bitslice; ++j) p.bitslice = descs[j].shard_len % kBsChunk == 0;
-    // the decode knob (hec_set_decode_vector_bytes) picks the 8-byte body for
-    // ragged decodes too, where every stripe has whole 2 KiB column ranges
-    p.narrow = decode && cfg.dec_vec_bytes == 8 && cfg.mode == 0;
-    for (uint32_t j = 0; j < n && p.narrow; ++j) p.narrow = descs[j].shard_len % kNarrowChunk == 0;
     // XCD eighths: the ragged decode +2% on the bench batch (with the no-op
     // skip +10% on the mixed workload, profiles/r02/ab_ragged_remap_skip.jsonl);
     // the bit-sliced ragged encode +2% at 512 mixed stripes, +7% at 4096 and
@@ -350,9 +344,6 @@ RaggedPick ragged_pick(const hec_stripe_desc* descs, uint32_t n, bool decode, co
 }
 
 const char* ragged_name(const RaggedPick& p, bool decode) {
-    if (decode && p.narrow)
-        return p.remap ? "rs104_ragged_narrow_kernel<DEC=true, 8 B per lane> (table lookup, XCD eighths)"
-                       : "rs104_ragged_narrow_kernel<DEC=true, 8 B per lane> (table lookup, dispatch order)";
     if (decode)
         return p.remap ? "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
                        : "rs104_ragged_kernel<DEC=true> (table lookup, dispatch order)";
@@ -374,7 +365,7 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     const LaunchConfig cfg = launch_config();
     const RaggedPick pick = ragged_pick(descs, n, decode, cfg);
     const bool bitslice = pick.bitslice;
-    const uint32_t chunk_bytes = pick.chunk_bytes();
+    const uint32_t chunk_bytes = bitslice ? kBsChunk : 4096;
     uint64_t n_blocks = 0;
     for (uint32_t j = 0; j < n; ++j) {
         const hec_stripe_desc& d = descs[j];
@@ -427,8 +418,6 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     }
     if (bitslice)
         HEC_HIP(launch_rs104_bs_ragged(ra, stream));
-    else if (pick.narrow)
-        HEC_HIP(launch_rs104_ragged_narrow(ra, stream));
     else
         HEC_HIP(launch_rs104_ragged(ra, decode, stream));
     HEC_HIP(hipEventRecord(slot.free, stream));

@@ -886,35 +886,6 @@ hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t str
     return hipSuccess;
 }
 
-// Ragged decode at 8 bytes per lane (every stripe length a multiple of
-// 2 KiB; hec_set_decode_vector_bytes 8, the default): one 2 KiB column range
-// of one stripe per workgroup, found through the workgroup map, the strided
-// batches' rs104_narrow_chunk body (0.9-1.7% faster than the 16-byte body
-// on the strided batch).
-__global__ __launch_bounds__(kThreads) void rs104_ragged_narrow_kernel(RaggedArgs a) {
-    const uint32_t blk = ragged_block(a);
-    const RaggedItem it = ragged_item(a, blk);
-    uint8_t* b = a.base + it.off;
-    rs104_narrow_chunk<true, false, u32x2>(b, b, it.shard_stride, it.shard_stride, blk - it.first_block, it.mask,
-                                           as_const(a.tabs), as_const(a.lut), a.bad_count);
-    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
-}
-
-hipError_t launch_rs104_ragged_narrow(const RaggedArgs& a, hipStream_t stream) {
-    for (uint64_t b0 = 0; b0 < a.n_blocks; b0 += kMaxLaunchBlocks) {  // see kMaxLaunchBlocks
-        RaggedArgs r = a;
-        r.block_base = uint32_t(b0);
-        if (b0 + kMaxLaunchBlocks < a.n_blocks) r.done_flag = nullptr;  // the last launch signals
-        const uint32_t nb = uint32_t(std::min<uint64_t>(kMaxLaunchBlocks, a.n_blocks - b0));
-        r.map_q8 = nb / 8;
-        r.map_r8 = nb % 8;
-        hipLaunchKernelGGL(rs104_ragged_narrow_kernel, dim3(nb), dim3(kThreads), 0, stream, r);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
 template <bool DEC, bool XORONLY, int TB>
 static hipError_t launch_rs104_tb(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
     const uint64_t chunk = uint64_t(TB) * kVecBytes;

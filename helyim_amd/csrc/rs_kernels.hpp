@@ -103,11 +103,6 @@ hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t str
 // the workgroup map has len / kBsChunk entries per stripe.
 constexpr uint32_t kBsChunk = 2 * kThreads * kVecBytes;  // 8 KiB
 hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream);
-// Ragged decode at 8 bytes per lane (not compact): every stripe's length a
-// multiple of kNarrowChunk bytes; the workgroup map has len / kNarrowChunk
-// entries per stripe.
-constexpr uint32_t kNarrowChunk = kThreads * 8;  // 2 KiB
-hipError_t launch_rs104_ragged_narrow(const RaggedArgs& a, hipStream_t stream);
 
 struct LaunchConfig {
     int vec_per_thread = 1;      // 16-byte vectors per lane per chunk (1, 2 or 4)

@@ -305,10 +305,8 @@ def test_kernel_name_follows_dispatch_under_every_knob():
 def test_ragged_kernel_name_follows_the_launch_choice():
     """hec_ragged_kernel_name comes from the ragged launch's own pick
     (ragged_pick in intervals.cpp): bit-sliced only when every length is a
-    multiple of 8 KiB, the 8-byte decode only when every length is a multiple
-    of 2 KiB (and the decode knob says 8), XCD eighths unless the
-    ragged-encode knob or the global xcd_remap (the global knob
-    now covers ragged encodes) is off."""
+    multiple of 8 KiB, XCD eighths unless the ragged-encode knob or the global
+    xcd_remap (the global knob now covers ragged encodes) is off."""
     import helyim_amd as H
     import helyim_amd.batch as B
     lib = H.lib
@@ -317,15 +315,7 @@ def test_ragged_kernel_name_follows_the_launch_choice():
     try:
         assert B.ragged_kernel_name(aligned, False) == "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
         assert B.ragged_kernel_name(odd, False) == "rs104_ragged_kernel<DEC=false> (table lookup, XCD eighths)"
-        # decodes: the 8-byte body where every length is a multiple of 2 KiB
-        narrow = "rs104_ragged_narrow_kernel<DEC=true, 8 B per lane> (table lookup, XCD eighths)"
-        assert B.ragged_kernel_name(aligned, True) == narrow
-        assert B.ragged_kernel_name(odd, True) == narrow
-        assert B.ragged_kernel_name(odd + [(0, 1024, 1000, 0x3FFF)], True) == \
-            "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
-        assert lib.hec_set_decode_vector_bytes(16) == 0
         assert B.ragged_kernel_name(aligned, True) == "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
-        assert lib.hec_set_decode_vector_bytes(8) == 0
         assert lib.hec_set_ragged_encode_remap(0) == 0
         assert B.ragged_kernel_name(aligned, False).endswith("(bit-sliced, dispatch order)")
         assert B.ragged_kernel_name(aligned, True).endswith("XCD eighths)")  # decodes follow the global knob
@@ -340,7 +330,6 @@ def test_ragged_kernel_name_follows_the_launch_choice():
         lib.hec_set_ragged_encode_remap(1)
         lib.hec_set_launch_config(1, 0, 1, 0)
         lib.hec_set_encode_kernel(1)
-        lib.hec_set_decode_vector_bytes(8)
 
 
 def test_host_alloc_multi_arguments_checked_before_device():

@@ -1,19 +1,22 @@
-# One GPU call: -m gpu tests, smoke(), default bench, the C-ABI bench,
-# rocprofv3 kernel trace + PMC passes of the bench (tools/profile.sh) and of
-# the mixed workload (tools/profile_mixed.sh), each step under its own time
-# limit, steps chained so the first failure ends the call. Outputs in
-# gpurun_out/$TAG; summaries: pmc_traffic.json, pmc_sq_wave_states.json,
-# pmc_mixed_workload.json.
+# One GPU call of round evidence, in the driver's order: the bench FIRST (the
+# driver's BENCH line is the first GPU process on its box), then the -m gpu
+# tests, smoke(), the C-ABI bench, rocprofv3 kernel trace + PMC passes of the
+# bench (tools/profile.sh) and of the mixed workload (tools/profile_mixed.sh),
+# and the counter calibration on known bytes (tools/pmc_calib.sh). Each step
+# under its own time limit, steps chained so the first failure ends the call.
+# Outputs in gpurun_out/$TAG; summaries: pmc_traffic.json (calibrated),
+# pmc_sq_wave_states.json, pmc_mixed_workload.json.
 set -e
 TAG=${1:-ev}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 120 ./build/cabi_bench > $OUT/cabi_bench.json 2>&1
 bash tools/profile.sh $TAG/prof
 bash tools/profile_mixed.sh $TAG/profmix
-python tools/pmc_summary.py $OUT/prof $OUT/pmc_traffic.json > /dev/null
+bash tools/pmc_calib.sh $TAG/calib
+python tools/pmc_summary.py $OUT/prof $OUT/pmc_traffic.json $OUT/calib > /dev/null
 python tools/sq_summary.py $OUT/prof/pmc_sq/run_counter_collection.csv $OUT/pmc_sq_wave_states.json > /dev/null
 python tools/pmc_mixed_summary.py $OUT/profmix $OUT/pmc_mixed_workload.json > /dev/null

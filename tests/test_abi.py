@@ -387,3 +387,37 @@ def test_host_encode_kernel_over_pcie():
     finally:
         lib.hec_set_host_encode_narrow(1)
         lib.hec_set_kernel_mode(0)
+
+
+def test_batch_base_alignment_helpers():
+    """bench.py --base-align: address_alignment is the
+    largest power of two dividing an address; empty_stripes refuses a
+    base_align that is not a power of two (and negative geometry) before it
+    allocates anything."""
+    import helyim_amd.batch as B
+    assert B.address_alignment(0x4000_0000) == 1 << 30
+    assert B.address_alignment(0x7F00_0020_0000) == 1 << 21
+    assert B.address_alignment(12) == 4
+    assert B.address_alignment(0) == 1 << 40
+    with pytest.raises(ValueError, match="power of two"):
+        B.empty_stripes(4, 14, 1 << 20, base_align=3 << 20)
+    with pytest.raises(ValueError):
+        B.empty_stripes(4, 14, 1 << 20, base_align=-1)
+
+
+def test_file_zero_copy_knob_and_counters():
+    """hec_set_file_zero_copy / hec_file_path_stats (the file layer's two
+    coding paths; DESIGN.md §5 "File level"): the knob takes any int, the
+    counters read without a device and do not move on calls that fail
+    before coding."""
+    import helyim_amd as H
+    lib = H.lib
+    a, b = ctypes.c_uint64(7), ctypes.c_uint64(7)
+    assert lib.hec_file_path_stats(ctypes.byref(a), ctypes.byref(b)) == 0
+    assert lib.hec_file_path_stats(None, None) == 0
+    before = (a.value, b.value)
+    for on in (1, 5, 0):
+        assert lib.hec_set_file_zero_copy(on) == 0
+    assert lib.hec_write_ec_files(b"/nonexistent/dir/vol") == 32  # HEC_ERR_IO: no .dat
+    assert lib.hec_file_path_stats(ctypes.byref(a), ctypes.byref(b)) == 0
+    assert (a.value, b.value) == before

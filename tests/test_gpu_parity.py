@@ -60,6 +60,48 @@ def test_generic_geometry_encode_reconstruct(gpu, k, m):
                 assert np.array_equal(got[i], ref[i]), (k, m, L, sorted(erased), i)
 
 
+def test_random_geometries_property_sweep(gpu):
+    """Seeded hypothesis sweep through the product's per-call API: random
+    geometries (k + m <= 256), shard lengths 1 B .. 40 KiB (both sides of the
+    16-byte alignment and of the table kernels' 4 KiB column range), random
+    erasure sets of 1..m shards and reconstruct_data, against the C oracle."""
+    from hypothesis import given, settings, HealthCheck, strategies as st
+    import helyim_amd as H
+    from oracle import corc
+
+    @settings(max_examples=60, deadline=None, derandomize=True,
+              suppress_health_check=[HealthCheck.too_slow])
+    @given(st.integers(1, 200), st.integers(1, 56), st.integers(1, 40 << 10), st.integers(0, 2**32 - 1),
+           st.booleans())
+    def check(k, m, L, seed, data_only):
+        rng = np.random.default_rng(seed)
+        n = k + m
+        rs, crs = H.ReedSolomon(k, m), corc.CReedSolomon(k, m)
+        data = [_rand(rng, L) for _ in range(k)]
+        sh = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+        ref = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+        rs.encode(sh)
+        crs.encode(ref)
+        for i in range(n):
+            assert np.array_equal(sh[i], ref[i]), (k, m, L, i)
+        e = int(rng.integers(1, m + 1))
+        erased = set(rng.choice(n, e, replace=False).tolist())
+        got = [None if i in erased else ref[i].copy() for i in range(n)]
+        if data_only:
+            rs.reconstruct_data(got)
+            for i in range(n):
+                if i < k or i not in erased:
+                    assert np.array_equal(got[i], ref[i]), (k, m, L, sorted(erased), i)
+                else:
+                    assert got[i] is None, (k, m, i)  # missing parity stays missing (upstream)
+        else:
+            rs.reconstruct(got)
+            for i in range(n):
+                assert np.array_equal(got[i], ref[i]), (k, m, L, sorted(erased), i)
+
+    check()
+
+
 @pytest.mark.parametrize("k,m", [(255, 1), (1, 255), (128, 128), (200, 56)])
 def test_widest_geometries_encode_reconstruct(gpu, k, m):
     """The widest codecs upstream accepts (data + parity = 256, the GF(2^8)

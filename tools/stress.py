@@ -9,6 +9,8 @@ Worker threads run, for --seconds, a random mix of:
   * file-level write_ec_files / rebuild_ec_files on small volumes,
   * device batches on a private torch stream,
   * device-resident ragged encode + reconstruct on a private stream,
+  * the staging census (hec_host_staging_stats) and the file layer's coding
+    path (hec_set_file_zero_copy) flipped under the other threads,
 every result checked bit-exact against the C oracle. Prints one JSON line.
 Measurement / test tool only.
 
@@ -167,12 +169,24 @@ def main():
         assert np.array_equal(dec, enc), "device_ragged reconstruct"
         note("device_ragged")
 
+    def knobs(rng):
+        # the staging census while other threads' host batches are in flight
+        # (it must not stall their leases), and the file layer's coding path
+        # flipped under the other threads' file calls (both paths give the
+        # same bytes, so every file check holds either way)
+        import ctypes
+        n, pin, dev = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        assert H.lib.hec_host_staging_stats(ctypes.byref(n), ctypes.byref(pin), ctypes.byref(dev)) == 0
+        assert 0 <= n.value <= 8, n.value
+        assert H.lib.hec_set_file_zero_copy(int(rng.integers(0, 2))) == 0
+        note("knobs")
+
     def worker(t_id):
         rng = np.random.default_rng(1000 + t_id)
         torch.cuda.set_device(0)
         stream = torch.cuda.Stream()
         ops = [percall, host_batch, ragged, lambda r: files(r, t_id), lambda r: device(r, stream),
-               lambda r: device_ragged(r, stream)]
+               lambda r: device_ragged(r, stream), knobs]
         while time.monotonic() < stop:
             op = ops[int(rng.integers(0, len(ops)))]
             try:

@@ -88,3 +88,21 @@ def test_bench_mixed_leg_verified_and_named_by_the_launcher(gpu):
     finally:
         H.lib.hec_set_ragged_encode_remap(1)
     assert B.ragged_kernel_name([(0, 4096, 4096, 0)], False).startswith("rs104_ragged_kernel<DEC=false>")
+
+
+@pytest.mark.gpu
+def test_bench_base_align_and_odd_shard_length():
+    """bench.py --base-align starts the batch at the
+    asked alignment and still verifies; a shard length that is not a multiple
+    of 8 checks parity and rebuilt shards without the seeded-data check
+    (no assertion after the timed region)."""
+    for extra, L, seeds in ((["--base-align", str(1 << 30)], 1 << 20, True),
+                            (["--shard-pad", "0"], 4096 + 4, False)):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stripes", "32", "--shard-len", str(L),
+                            "--steps", "2", "--warmup", "1", "--no-extras", "--no-packed", "--no-cpu-baseline",
+                            *extra], capture_output=True, text=True, timeout=300, cwd=ROOT)
+        assert p.returncode == 0, p.stderr[-3000:]
+        d = json.loads([x for x in p.stdout.splitlines() if x.strip()][-1])
+        assert d["verified"] is True and d["verification"]["data_seeds_checked"] is seeds
+        if extra[0] == "--base-align":
+            assert d["config"]["base_alignment"] >= 1 << 30

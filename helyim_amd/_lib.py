@@ -98,6 +98,7 @@ SIGNATURES = {
     "hec_set_ragged_encode_remap": (_I, [_I]),
     "hec_set_host_zero_copy": (_I, [_I]),
     "hec_set_file_zero_copy": (_I, [_I]),
+    "hec_set_bitslice_vector_bytes": (_I, [_I]),
     "hec_file_path_stats": (_I, [ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "hec_set_host_encode_narrow": (_I, [_I]),
     "hec_host_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),

@@ -809,6 +809,12 @@ int hec_set_encode_vector_bytes(int bytes) {
     return HEC_OK;
 }
 
+int hec_set_bitslice_vector_bytes(int bytes) {
+    if (bytes != 8 && bytes != 16) return fail(HEC_ERR_INVALID_ARGUMENT, "bit-sliced vector bytes must be 8 or 16");
+    update_launch_config([&](LaunchConfig& c) { c.bs_vec_bytes = bytes; });
+    return HEC_OK;
+}
+
 int hec_set_encode_kernel(int kind) {
     if (kind != 0 && kind != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0 or 1");
     update_launch_config([&](LaunchConfig& c) { c.bitslice = kind; });

@@ -716,45 +716,78 @@ __global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
 // ---------------------------------------------------------------------------
 // One 2*TB*16-byte column range (`chunk`) of one stripe: inputs 0..9 at in_b,
 // parity 0..3 at out_b.
-template <int TB, typename OffT = uint64_t>
+// VB = 16: two dwordx4 per lane per shard, TB*16 apart; VB = 8 (measurement,
+// hec_set_bitslice_vector_bytes): four dwordx2 per lane per shard, TB*8 apart,
+// the same 2*TB*16-byte column range. Each output byte depends only on the
+// input bytes of its own column, so the planes only need the stores to use
+// the loads' byte positions.
+template <int TB, typename OffT = uint64_t, int VB = 16>
 __device__ __forceinline__ void rs104_bs_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
                                                uint64_t out_shard, uint32_t chunk) {
-    constexpr int K = 10, R = 4;
-    const OffT o0 = OffT(chunk) * OffT(TB * 2 * kVecBytes) + OffT(threadIdx.x * kVecBytes);
-    const OffT o1 = o0 + OffT(TB * kVecBytes);
-    u32x4 d[K][2];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        d[i][0] = load_at(in_b + uint64_t(i) * in_shard, o0);
-        d[i][1] = load_at(in_b + uint64_t(i) * in_shard, o1);
-    }
+    constexpr int K = 10, R = 4, NV = 32 / VB;  // vectors per lane per shard
+    static_assert(VB == 16 || VB == 8, "bit-sliced lanes load 16 or 8 bytes at a time");
+    const OffT base = OffT(chunk) * OffT(TB * 2 * kVecBytes) + OffT(threadIdx.x * VB);
     uint32_t p[K * 8];
+    if constexpr (VB == 16) {
+        u32x4 d[K][2];
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            p[8 * i + w] = d[i][0][w];
-            p[8 * i + 4 + w] = d[i][1][w];
+        for (int i = 0; i < K; ++i) {
+            d[i][0] = load_at(in_b + uint64_t(i) * in_shard, base);
+            d[i][1] = load_at(in_b + uint64_t(i) * in_shard, base + OffT(TB * 16));
         }
-        transpose8(p + 8 * i);
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                p[8 * i + w] = d[i][0][w];
+                p[8 * i + 4 + w] = d[i][1][w];
+            }
+    } else {
+        u32x2 d[K][NV];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                d[i][v] = __builtin_nontemporal_load(
+                    (const __attribute__((address_space(1))) u32x2*)((gcu8p)(in_b + uint64_t(i) * in_shard) + base +
+                                                                     OffT(v * TB * 8)));
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                p[8 * i + 2 * v] = d[i][v][0];
+                p[8 * i + 2 * v + 1] = d[i][v][1];
+            }
     }
+#pragma unroll
+    for (int i = 0; i < K; ++i) transpose8(p + 8 * i);
     uint32_t q[R * 8];
     rs104_encode_planes(p, q);
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         transpose8(q + 8 * j);
-        store_at(out_b + uint64_t(j) * out_shard, o0, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]});
-        store_at(out_b + uint64_t(j) * out_shard, o1, u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]});
+        if constexpr (VB == 16) {
+            store_at(out_b + uint64_t(j) * out_shard, base, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]});
+            store_at(out_b + uint64_t(j) * out_shard, base + OffT(TB * 16),
+                     u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]});
+        } else {
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                __builtin_nontemporal_store(
+                    u32x2{q[8 * j + 2 * v], q[8 * j + 2 * v + 1]},
+                    (__attribute__((address_space(1))) u32x2*)((gu8p)(out_b + uint64_t(j) * out_shard) + base +
+                                                               OffT(v * TB * 8)));
+        }
     }
 }
 
-template <int TB, bool FAST>
+template <int TB, bool FAST, int VB = 16>
 __global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
     uint32_t stripe, chunk;
     fast_item<FAST>(a, a.chunks_per_stripe, stripe, chunk);
     using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
-    rs104_bs_chunk<TB, OffT>(a.in_base + uint64_t(stripe) * a.in_stripe,
-                             a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, chunk);
+    rs104_bs_chunk<TB, OffT, VB>(a.in_base + uint64_t(stripe) * a.in_stripe,
+                                 a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, chunk);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
@@ -832,7 +865,10 @@ static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStrea
     a.chunk_rot = uint32_t(cfg.chunk_rot);
     set_fast_map(a, a.n_items, a.chunks_per_stripe);
     const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    if (fast_map_ok(cfg, a.len))
+    if (fast_map_ok(cfg, a.len) && cfg.bs_vec_bytes == 8)
+        hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, true, 8>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream,
+                           a);
+    else if (fast_map_ok(cfg, a.len))
         hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, true>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
     else
         hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, false>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
@@ -941,7 +977,8 @@ static bool rs104_bitslice_ok(uint64_t len, const LaunchConfig& cfg);
 static Rs104Pick rs104_pick(uint64_t len, uint64_t n_stripes, bool dec, const LaunchConfig& cfg) {
     const uint64_t items = (len + 4095) / 4096 * n_stripes;
     if (!rs104_fast_ok(len, cfg) || items > kMaxLaunchBlocks) return {Rs104Kind::Apply, 16};
-    if (!dec && rs104_bitslice_ok(len, cfg)) return {Rs104Kind::Bitslice, 16};
+    if (!dec && rs104_bitslice_ok(len, cfg))
+        return {Rs104Kind::Bitslice, cfg.bs_vec_bytes == 8 && fast_map_ok(cfg, len) ? 8 : 16};
     const int vb = dec ? cfg.dec_vec_bytes : cfg.enc_vec_bytes;
     const uint64_t narrow = uint64_t(kThreads) * uint64_t(vb);  // column range per workgroup
     // (launch_apply sizes its stripe ranges for 4 KiB chunks; a narrow launch
@@ -1018,7 +1055,8 @@ static const char* rs104_name(const Rs104Pick& p, bool dec, bool xo) {
     switch (p.kind) {
         case Rs104Kind::Apply:
             return xo ? "rs_apply_kernel<10, XORONLY=true> (diagnostic)" : "rs_apply_kernel<10> (table lookup)";
-        case Rs104Kind::Bitslice: return "rs104_bs_encode_kernel (bit-sliced)";
+        case Rs104Kind::Bitslice:
+            return p.vb == 8 ? "rs104_bs_encode_kernel (bit-sliced, 8 B loads)" : "rs104_bs_encode_kernel (bit-sliced)";
         case Rs104Kind::Narrow:
             if (p.vb == 8)
                 return dec ? (xo ? "rs104_narrow_kernel<DEC=true, XORONLY=true, 8 B per lane> (diagnostic)"

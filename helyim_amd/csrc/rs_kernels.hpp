@@ -117,6 +117,8 @@ struct LaunchConfig {
                                  // per workgroup, on shard lengths a multiple of 2 KiB), 16 or 4 (speed only)
     int enc_vec_bytes = 16;      // RS(10,4) table encode bytes per lane per shard: 16 (default), 8 or 4 (speed only)
     int ragged_encode_remap = 1; // 1: XCD eighths for ragged encodes (default; 0 = dispatch order; speed only)
+    int bs_vec_bytes = 16;       // bit-sliced encode loads / stores: 16 (two dwordx4 per lane per shard,
+                                 // default) or 8 (four dwordx2; same column range; speed only)
     int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
                                  // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
                                  // multiply (speed only)

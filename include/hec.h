@@ -452,6 +452,10 @@ int hec_set_encode_vector_bytes(int bytes);
  * XOR program; the default), 0 = table-lookup GF multiply. Both give identical
  * parity (parity-tested); speed only. Returns HEC_OK. */
 int hec_set_encode_kernel(int kind);
+/* Bit-sliced encode memory access (measurement): 16 = two 16-byte vectors per
+ * lane per shard (default), 8 = four 8-byte vectors over the same column
+ * range. Identical parity; speed only. HEC_ERR_INVALID_ARGUMENT otherwise. */
+int hec_set_bitslice_vector_bytes(int bytes);
 /* Ragged device encodes (hec_gpu_encode_ragged): 1 = the workgroups of one
  * XCD take a contiguous eighth of the launch's column ranges, as the decodes
  * do with xcd_remap 1 (default; 3-9% faster on the mixed workload, DESIGN.md

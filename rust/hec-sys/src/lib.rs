@@ -200,6 +200,7 @@ extern "C" {
     pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;
     pub fn hec_set_host_zero_copy(on: c_int) -> c_int;
     pub fn hec_set_file_zero_copy(on: c_int) -> c_int;
+    pub fn hec_set_bitslice_vector_bytes(bytes: c_int) -> c_int;
     pub fn hec_file_path_stats(zero_copy_calls: *mut u64, fallbacks: *mut u64) -> c_int;
     pub fn hec_set_host_encode_narrow(on: c_int) -> c_int;
     pub fn hec_host_encode_kernel_name(shard_len: u64) -> *const c_char;

@@ -318,6 +318,31 @@ def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):
     return t
 
 
+@pytest.mark.parametrize("S,L,pad", [(37, 3 * 8192, 0), (300, 8192, 64 << 10), (5, 1 << 20, 0), (3, 1 << 20, 16)])
+def test_bitslice_vector_bytes_identical(gpu, S, L, pad):
+    """hec_set_bitslice_vector_bytes(8) (four dwordx2 per lane per shard over
+    the same column range) writes the oracle's parity, like the default 16,
+    packed and padded (a 16-byte pad: shard bases only 16-byte aligned)."""
+    import torch
+    import helyim_amd as H
+    import helyim_amd.batch as B
+    from oracle import corc
+    t = B.empty_stripes(S, 14, L, shard_pad=pad)
+    B.fill_stripes_splitmix(t, 10, O.STRIPE_SEED_BASE)
+    try:
+        for vb in (8, 16):
+            assert H.lib.hec_set_bitslice_vector_bytes(vb) == 0
+            want = "rs104_bs_encode_kernel (bit-sliced, 8 B loads)" if vb == 8 else "rs104_bs_encode_kernel (bit-sliced)"
+            assert H.lib.hec_encode_kernel_name(L).decode() == want
+            t[:, 10:] = 0
+            B.encode_batch(H.ReedSolomon(10, 4), t)
+            torch.cuda.synchronize()
+            assert corc.check_device_batch(t) == [], vb
+    finally:
+        H.lib.hec_set_bitslice_vector_bytes(16)
+    assert H.lib.hec_set_bitslice_vector_bytes(4) != 0
+
+
 def test_fill_splitmix_matches_oracle(gpu):
     S, L = 3, 4097
     t = _stripes(S, L).cpu().numpy()

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--encs", default="0", help="encode kernel: 0 table lookup, 1 bit-sliced")
     ap.add_argument("--decvecs", default="8", help="decode bytes per lane (8 default, 16, 4)")
     ap.add_argument("--encvecs", default="16", help="table-encode bytes per lane (16 default, 8, 4)")
+    ap.add_argument("--bsvecs", default="16", help="bit-sliced encode load/store bytes per lane (16 default, 8)")
     ap.add_argument("--pad", type=int, default=64 << 10,
                     help="extra bytes between shards (default: the bench's batch.SHARD_PAD)")
     ap.add_argument("--stripe-pad", type=int, default=0, help="extra bytes between stripes (shards stay 1 MiB apart)")
@@ -62,13 +63,14 @@ def main():
     ints = lambda x: [int(y) for y in x.split(",")]
     configs = list(itertools.product(ints(args.modes), ints(args.vecs), ints(args.blocks), ints(args.remaps),
                                      ints(args.bpcs), ints(args.parts), ints(args.rots), ints(args.wgs),
-                                     ints(args.encs), ints(args.decvecs), ints(args.encvecs)))
+                                     ints(args.encs), ints(args.decvecs), ints(args.encvecs), ints(args.bsvecs)))
     res = {c: {"enc": [], "dec": []} for c in configs}
     s = torch.cuda.current_stream()
     for _ in range(args.rounds):
         for c in configs:
-            mode, v, b, rm, bpc, parts, rot, wg, enc, dv, ev = c
+            mode, v, b, rm, bpc, parts, rot, wg, enc, dv, ev, bv = c
             H.lib.hec_set_encode_kernel(enc)
+            H.lib.hec_set_bitslice_vector_bytes(bv)
             H.lib.hec_set_decode_vector_bytes(dv)
             H.lib.hec_set_encode_vector_bytes(ev)
             H.lib.hec_set_kernel_mode(mode)
@@ -92,6 +94,7 @@ def main():
     H.lib.hec_set_workgroup_size(256)
     H.lib.hec_set_decode_vector_bytes(8)
     H.lib.hec_set_encode_vector_bytes(16)
+    H.lib.hec_set_bitslice_vector_bytes(16)
     B.set_launch_config()
     nbytes = S * 14 * L
     for c in configs:
@@ -99,7 +102,7 @@ def main():
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "pad": args.pad, "stripe_pad": args.stripe_pad,
                           "tile": args.tile,
                           "mode": ["gf", "xor_ceiling"][c[0]], "vec_per_thread": c[1], "max_blocks": c[2],
-                          "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7], "encode_kernel": ["table", "bitslice"][c[8]], "dec_vec_bytes": c[9], "enc_vec_bytes": c[10],
+                          "xcd_remap": c[3], "blocks_per_cu": c[4], "xcd_parts": c[5], "chunk_rot": c[6], "wg_threads": c[7], "encode_kernel": ["table", "bitslice"][c[8]], "dec_vec_bytes": c[9], "enc_vec_bytes": c[10], "bs_vec_bytes": c[11],
                           "enc_ms_med": round(float(np.median(enc)), 3), "enc_ms_min": round(float(enc.min()), 3),
                           "enc_GBps": round(nbytes / np.median(enc) / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 3),

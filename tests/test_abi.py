@@ -210,6 +210,12 @@ def test_kernel_selection_knobs_host_only():
         assert lib.hec_set_kernel_mode(1) == 0
         assert "diagnostic" in lib.hec_encode_kernel_name(1 << 20).decode()
         assert lib.hec_set_kernel_mode(2) != 0
+        assert lib.hec_set_kernel_mode(0) == 0
+        assert lib.hec_set_bitslice_vector_bytes(8) == 0
+        assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced, 8 B loads)"
+        assert lib.hec_set_bitslice_vector_bytes(4) != 0 and lib.hec_set_bitslice_vector_bytes(16) == 0
+        assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced)"
+        assert lib.hec_set_kernel_mode(1) == 0
         assert lib.hec_set_host_zero_copy(0) == 0 and lib.hec_set_host_zero_copy(1) == 0
         assert lib.hec_set_kernel_mode(0) == 0 and lib.hec_set_workgroup_size(256) == 0
         # the name follows the dispatch predicate: 4 vectors per lane or a grid
@@ -228,6 +234,7 @@ def test_kernel_selection_knobs_host_only():
         lib.hec_set_workgroup_size(256)
         lib.hec_set_encode_kernel(1)
         lib.hec_set_launch_config(1, 0, 1, 0)
+        lib.hec_set_bitslice_vector_bytes(16)
 
 
 def test_strided_batch_geometry_checked_before_device():

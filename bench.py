@@ -97,6 +97,21 @@ def job_throughput(payload_bytes_per_rank_step: float, steps: int, world: int, t
     return payload_bytes_per_rank_step * steps * world / t_job / 2**30
 
 
+def scaling_fields(value: float, world: int, per_rank: list) -> dict:
+    """The per-GPU view of a multi-rank line (the
+    1/2/4/8-GPU curve read as per-GPU efficiency against the 1-GPU run):
+    per_gpu_GiB_s = value / N; rank_spread = slowest / fastest rank's step
+    (its own HIP-event encode + decode ms); each rank's encode / decode
+    roofline fraction. per_rank entries: {"rank", "step_ms", "encode_frac",
+    "decode_frac"} (fractions None in the GPU-free dry run)."""
+    steps = [r["step_ms"] for r in per_rank]
+    return {"per_gpu_GiB_s": round(value / world, 4),
+            "rank_spread": round(max(steps) / min(steps), 4) if min(steps) > 0 else None,
+            "per_rank_frac": [{"rank": r["rank"], "step_ms": round(r["step_ms"], 4),
+                               "encode_frac": r.get("encode_frac"), "decode_frac": r.get("decode_frac")}
+                              for r in per_rank]}
+
+
 def aggregate_host_path(per_rank: list) -> dict:
     """Whole-node host-path rate from per-rank legs run at the same time:
     bytes of all ranks / the wall-clock window from the first rank's start to
@@ -708,7 +723,7 @@ def dry_run(args, world: int, rank: int, local_rank: int) -> int:
     t_job = reduce_max(wall, world)
     per_rank = gather({"rank": rank, "local_rank": local_rank, "world_size": int(os.environ.get("WORLD_SIZE", "1")),
                        "seed_base": rank_seed_base(rank), "wall_s": wall, "pid": os.getpid(),
-                       "masks_head": erasure_masks(4, rank).tolist()}, world)
+                       "step_ms": step * 1e3, "masks_head": erasure_masks(4, rank).tolist()}, world)
     # host legs: stand-in records with the real records' shape (rank r moves
     # (r + 1) GiB in (r + 1) x dry_step_ms per phase), assembled as run_rank does
     barrier()
@@ -735,6 +750,7 @@ def dry_run(args, world: int, rank: int, local_rank: int) -> int:
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(t_job / args.steps * 1e3, 4), "scaling": "weak", "verified": chk_ok,
                "rank_seed_bases": [r["seed_base"] for r in per_rank], "ranks": per_rank}
+        out.update(scaling_fields(out["value"], world, per_rank))
         out.update(extras)
         if not args.no_cpu_baseline:
             out.update(cpu_baseline_legs(args.cpu_seconds, os.sched_getaffinity(0), stand_in=True))
@@ -826,16 +842,19 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
     if args.shard_pad and not args.no_packed:
         torch.cuda.empty_cache()
         packed = packed_layout_pass(rs, S, L, masks, rank, max(3, args.steps // 2))
+    enc_bytes = S * N_TOTAL * L                      # read 10 L + write 4 L per stripe
+    dec_bytes = S * (K_DATA + 4) * L                 # read 10 survivors + write 4 erased
     per_rank = gather({"rank": rank, "device": device, "seed_base": rank_seed_base(rank), "numa": numa,
                        "verification": verification,
                        "wall_s": round(wall, 6), "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
-                       "encode_ms_median": round(enc_med, 4), "decode_ms_median": round(dec_med, 4)},
+                       "encode_ms_median": round(enc_med, 4), "decode_ms_median": round(dec_med, 4),
+                       "step_ms": enc_ms + dec_ms,
+                       "encode_frac": round(enc_bytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "decode_frac": round(dec_bytes / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
                       world)
     enc_ms = max(r["encode_ms"] for r in per_rank)
     dec_ms = max(r["decode_ms"] for r in per_rank)
 
-    enc_bytes = S * N_TOTAL * L                      # read 10 L + write 4 L per stripe
-    dec_bytes = S * (K_DATA + 4) * L                 # read 10 survivors + write 4 erased
     payload = 2 * S * K_DATA * L                     # data-payload bytes per step (encode + decode)
     value = job_throughput(payload, args.steps, world, t_job)
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
@@ -924,6 +943,7 @@ def run_rank(args, world: int, rank: int, local_rank: int) -> int:
             "verification": verification,
             "ranks": per_rank,
         }
+        out.update(scaling_fields(out["value"], world, per_rank))
         out.update(extras)
         if not args.no_cpu_baseline:  # every world size; the other ranks wait at main()'s closing barrier
             out.update(cpu_baseline_legs(args.cpu_seconds, allowed))

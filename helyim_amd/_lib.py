@@ -87,25 +87,13 @@ SIGNATURES = {
     "hec_ec_volume_delete_needle": (_I, [_P, _U64]),
     "hec_ec_volume_read_needle": (_I, [_P, _U64, _P, _S, ctypes.POINTER(_S)]),
     "hec_ec_volume_read_needles": (_I, [_P, _P, _S, _P, _S, _P, _P]),
-    "hec_set_launch_config": (_I, [_I, ctypes.c_long, _I, _I]),
-    "hec_set_kernel_mode": (_I, [_I]),
     "hec_set_host_staging": (_I, [ctypes.c_uint64]),
     "hec_set_completion_signal": (_I, [ctypes.c_uint64]),
-    "hec_set_workgroup_size": (_I, [_I]),
     "hec_set_decode_vector_bytes": (_I, [_I]),
-    "hec_set_encode_vector_bytes": (_I, [_I]),
-    "hec_set_encode_kernel": (_I, [_I]),
-    "hec_set_ragged_encode_remap": (_I, [_I]),
     "hec_set_host_zero_copy": (_I, [_I]),
-    "hec_set_file_zero_copy": (_I, [_I]),
-    "hec_set_bitslice_vector_bytes": (_I, [_I]),
-    "hec_file_path_stats": (_I, [ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
-    "hec_set_host_encode_narrow": (_I, [_I]),
     "hec_host_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hec_host_zero_copy_view": (_I, [_P, _U64, ctypes.POINTER(_I)]),
     "hec_host_staging_stats": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
-    "hec_set_xcd_parts": (_I, [_I]),
-    "hec_set_chunk_rotation": (_I, [_I]),
     "hec_version": (ctypes.c_char_p, []),
     "hec_device_count": (_I, [ctypes.POINTER(_I)]),
     "hec_set_device": (_I, [_I]),

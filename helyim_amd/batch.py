@@ -287,9 +287,3 @@ def fill_stripes_splitmix(t: torch.Tensor, data_shards: int, seed_base: int, str
         raise ValueError("a padded batch needs shard_len % 8 == 0 (the generator emits 8-byte words)")
     for i in range(data_shards):
         fill_splitmix(t[:, i], L, shard_seed(seed_base, i, L), stream)
-
-
-def set_launch_config(vec_per_thread: int = 1, max_blocks: int = 0, xcd_remap: int = 1,
-                      blocks_per_cu: int = 0) -> None:
-    """Process-wide kernel launch configuration (speed only; bytes identical)."""
-    check(lib.hec_set_launch_config(vec_per_thread, max_blocks, xcd_remap, blocks_per_cu))

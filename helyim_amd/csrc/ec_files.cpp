@@ -14,7 +14,6 @@
 // all 14 (or the rebuilt) shard files in parallel on the pool. Reading job
 // k+1, the GPU work of job k and the writes of job k-1 overlap.
 #include <fcntl.h>
-#include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/vfs.h>
 #include <sys/uio.h>
@@ -350,10 +349,6 @@ class FilePipeline {
         return code ? fail_with(code, detail, values) : HEC_OK;
     }
     ErrorSlot& errors() { return err_; }
-    // The zero-copy file path borrows the I/O pool and slot 0's stream (the
-    // lease makes this call the pipeline's only user).
-    Pool& pool() { return pool_; }
-    hipStream_t stream0() const { return slots_[0].stream; }
 
    private:
     int gpu(Slot& s, const Job& job) {
@@ -485,14 +480,14 @@ std::shared_future<void> preallocate_async(const int* fds, int n, uint64_t bytes
 // existing multi-GiB shard file frees its pages, which is slow one file at a
 // time. Same files and flags as the reference's sequential opens; on failure
 // the lowest-numbered failing file is reported.
-int open_outputs(const std::string& base, const bool* which, Fd* out, int mode = O_WRONLY) {
+int open_outputs(const std::string& base, const bool* which, Fd* out) {
     std::vector<std::thread> th;
     int err[N];
     for (int i = 0; i < N; ++i) {
         err[i] = 0;
         if (which[i])
             th.emplace_back([&, i] {
-                out[i].fd = ::open(shard_name(base, i).c_str(), mode | O_CREAT | O_TRUNC, 0644);
+                out[i].fd = ::open(shard_name(base, i).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
                 if (out[i].fd < 0) err[i] = errno;
             });
     }
@@ -510,169 +505,6 @@ void add_reads(std::vector<ReadSeg>& v, int fd, uint64_t host_off, uint64_t len,
     uint64_t per = std::max<uint64_t>(1, (units + parts - 1) / parts) * unit;
     for (uint64_t o = 0; o < len; o += per) v.push_back({fd, host_off + o, std::min(per, len - o), file_off + o});
 }
-
-// ---------------------------------------------------------------------------
-// Zero copy through the page cache (opt-in: hec_set_file_zero_copy(1)).
-// ---------------------------------------------------------------------------
-// The staged pipeline above copies every byte twice on the CPU: pread of the
-// .dat into pinned staging, pwritev of all 14 shards out of it (a 12 GiB
-// volume: 28.8 GiB of memcpy on 13-14 of the box's 16 CPUs while the GPU
-// waits 0.05 s; profiles/r04/file_stages_fs/). Here the files themselves are
-// the GPU's operands: the .dat is mmap'd read-only, the shard files the GPU
-// writes are ftruncate'd to their final size and mmap'd shared at a fixed
-// stride in one VA reservation, and both are registered with the GPU
-// (hipHostRegister on the page-cache pages), so the kernels stream .dat pages
-// and write parity / rebuilt pages over PCIe in place. The 10 data shards of
-// an encode are byte copies of .dat blocks: the CPU pwritev()s them straight
-// out of the .dat mapping while the GPU codes. Left on the CPU: one copy of
-// the data and the zeroing of fresh output pages.
-// Measured and NOT the default (profiles/r05/file_stages_b.json, a 12 GiB
-// volume in /dev/shm, alternating calls): zero copy 2.30-2.43 s encode /
-// 1.28-1.71 s rebuild against 0.51-0.54 / 0.33-0.40 s staged, on 16.3-17.3
-// against 7.0-7.7 CPU-seconds. Registering 4 KiB page-cache pages costs more
-// than copying them: populate + register 0.73-1.14 s and unregister 0.46-0.49 s
-// per 16.8 GiB, against ~0.45 s for the staged pipeline's whole pread.
-std::atomic<int>& file_zero_copy_mode() {
-    static std::atomic<int> m{0};
-    return m;
-}
-constexpr int kFallback = -1000;  // internal status: registration refused, take the staged path
-constexpr int kNoRows = -1001;    // internal status: no whole row to map (a .dat below one row): staged
-// Calls that coded zero copy / that fell back to the staged path (hec_file_path_stats).
-std::atomic<uint64_t> g_zc_calls{0}, g_zc_fallbacks{0};
-constexpr uint64_t kRegChunk = 256ull << 20;  // registration unit (parallel over the I/O pool)
-#ifndef MADV_POPULATE_READ
-#define MADV_POPULATE_READ 22
-#endif
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23
-#endif
-
-bool regular_file(int fd) {
-    struct stat st;
-    return ::fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
-}
-
-uint64_t page_round(uint64_t n) {
-    static const uint64_t pg = uint64_t(::sysconf(_SC_PAGESIZE));
-    return (n + pg - 1) / pg * pg;
-}
-
-// Stage clock of the zero-copy path (HEC_FILE_TRACE=1, stderr).
-struct ZcClock {
-    int64_t t0 = StageClock::now(), map = 0, reg = 0, cpu = 0, gpu = 0, unreg = 0;
-    void print(const char* what) const {
-        static const bool trace = std::getenv("HEC_FILE_TRACE") != nullptr;
-        if (trace)
-            std::fprintf(stderr, "hec file zero-copy %s: map %.3f s, populate+register %.3f s, cpu copies %.3f s, "
-                                 "gpu wait %.3f s, unregister+unmap %.3f s\n",
-                         what, map * 1e-9, reg * 1e-9, cpu * 1e-9, gpu * 1e-9, unreg * 1e-9);
-    }
-};
-
-// One VA reservation holding up to 14 file mappings at a fixed stride, and
-// the GPU registrations over them. Destruction unregisters (the GPU must be
-// idle by then: callers synchronise their stream first) and unmaps.
-class MappedSet {
-   public:
-    MappedSet(Pool& pool, int n_slots, uint64_t stride) : pool_(pool), n_(n_slots), stride_(stride) {}
-    ~MappedSet() { release(); }
-    int reserve() {
-        void* p = ::mmap(nullptr, size_t(n_) * stride_, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-        if (p == MAP_FAILED) return fail_errno(HEC_ERR_IO, "mmap reserve", errno);
-        base_ = static_cast<uint8_t*>(p);
-        return HEC_OK;
-    }
-    // Map fd's [0, len) at slot i (len > 0).
-    int map(int i, int fd, uint64_t len, bool writable) {
-        void* p = ::mmap(base_ + uint64_t(i) * stride_, page_round(len), writable ? PROT_READ | PROT_WRITE : PROT_READ,
-                         MAP_SHARED | MAP_FIXED, fd, 0);
-        if (p == MAP_FAILED) return fail_errno(HEC_ERR_IO, "mmap shard file", errno);
-        ranges_.push_back({base_ + uint64_t(i) * stride_, page_round(len), writable});
-        return HEC_OK;
-    }
-    uint8_t* slot(int i) const { return base_ + uint64_t(i) * stride_; }
-    // Populate and register every mapped range with the GPU, in kRegChunk
-    // pieces on the pool. HEC_OK with *dev = the device address of base (every
-    // piece must sit at the same host -> device offset, so one launch can
-    // span pieces), kFallback if the runtime refuses file pages, or an error.
-    int register_all(uint8_t** dev) {
-        struct Piece {
-            uint8_t* p;
-            uint64_t len;
-            bool rw;
-        };
-        std::vector<Piece> pieces;
-        for (const Range& r : ranges_)
-            for (uint64_t o = 0; o < r.len; o += kRegChunk) pieces.push_back({r.p + o, std::min(kRegChunk, r.len - o), r.rw});
-        std::vector<int64_t> delta(pieces.size(), 0);
-        std::vector<char> ok(pieces.size(), 0);
-        std::string why;
-        std::mutex why_mu;
-        std::vector<std::function<void()>> tasks;
-        for (size_t t = 0; t < pieces.size(); ++t)
-            tasks.push_back([&, t] {
-                const Piece& pc = pieces[t];
-                // fault the pages in from this thread (fresh output pages are
-                // zeroed here, in parallel, not inside the runtime's walk)
-                (void)::madvise(pc.p, pc.len, pc.rw ? MADV_POPULATE_WRITE : MADV_POPULATE_READ);
-                unsigned flags = hipHostRegisterMapped | (pc.rw ? 0u : unsigned(hipHostRegisterReadOnly));
-                hipError_t e = hipHostRegister(pc.p, pc.len, flags);
-                if (e != hipSuccess && !pc.rw) {  // runtimes without the read-only flag
-                    (void)hipGetLastError();
-                    e = hipHostRegister(pc.p, pc.len, hipHostRegisterMapped);
-                }
-                void* d = nullptr;
-                if (e == hipSuccess) {
-                    ok[t] = 1;
-                    e = hipHostGetDevicePointer(&d, pc.p, 0);
-                }
-                if (e != hipSuccess) {
-                    (void)hipGetLastError();
-                    std::lock_guard<std::mutex> g(why_mu);
-                    why = std::string("hipHostRegister of file pages: ") + hipGetErrorString(e);
-                    return;
-                }
-                delta[t] = static_cast<uint8_t*>(d) - pc.p;
-            });
-        pool_.run_all(tasks);
-        for (size_t t = 0; t < pieces.size(); ++t)
-            if (ok[t]) registered_.push_back(pieces[t].p);
-        if (!why.empty()) {
-            set_detail(why);
-            return kFallback;
-        }
-        for (size_t t = 1; t < pieces.size(); ++t)
-            if (delta[t] != delta[0]) {
-                set_detail("registered file pages are not contiguous in the GPU's address space");
-                return kFallback;
-            }
-        *dev = base_ + (pieces.empty() ? 0 : delta[0]);
-        return HEC_OK;
-    }
-    void release() {
-        std::vector<std::function<void()>> tasks;
-        for (void* p : registered_) tasks.push_back([p] { (void)hipHostUnregister(p); });
-        pool_.run_all(tasks);
-        registered_.clear();
-        if (base_) ::munmap(base_, size_t(n_) * stride_);
-        base_ = nullptr;
-        ranges_.clear();
-    }
-
-   private:
-    struct Range {
-        uint8_t* p;
-        uint64_t len;
-        bool rw;
-    };
-    Pool& pool_;
-    int n_;
-    uint64_t stride_;
-    uint8_t* base_ = nullptr;
-    std::vector<Range> ranges_;
-    std::vector<void*> registered_;
-};
 
 // One job of the staged pipeline over b whole small rows at .dat offset
 // `processed` (encoder.rs:228-239): whole rows are contiguous in .dat.
@@ -698,144 +530,6 @@ Job small_rows_job(int dat_fd, const Fd* out, const DevicePlanSet* enc, uint64_t
     return job;
 }
 
-// write_ec_files over the page cache. The rows wholly inside the .dat are
-// coded zero copy; a last partial small row (zero-padded past EOF,
-// encoder.rs:169-189) goes through the staged pipeline. Shard files are
-// sized up front (ftruncate) to the reference's final size.
-int write_zero_copy(FilePipeline& pipe, int dat_fd, uint64_t dat_size, const Fd* out, const DevicePlanSet* enc,
-                    uint64_t large, uint64_t small, uint64_t n_large, uint64_t n_small) {
-    ZcClock clk;
-    const uint64_t large_row = large * K, small_row = small * K;
-    const uint64_t shard_size = n_large * large + n_small * small;
-    const uint64_t full_small = std::min(n_small, (dat_size - n_large * large_row) / small_row);
-    const uint64_t mapped = n_large * large_row + full_small * small_row;  // .dat bytes coded zero copy
-    if (mapped == 0) return kNoRows;
-    if (!regular_file(dat_fd)) return kFallback;
-    // the parity files get their final size now (mapped pages need it); the
-    // data shards grow by their writes. Anything but regular files (a device
-    // node, a pipe) takes the staged path, which reports their errors as the
-    // reference's writes would.
-    for (int j = 0; j < M; ++j)
-        if (!regular_file(out[K + j].fd) || ::ftruncate(out[K + j].fd, off_t(shard_size)) != 0) return kFallback;
-    // slot 0: the .dat rows; slots 1..4: the parity files at stride ps
-    const uint64_t ps = page_round(std::max(shard_size, mapped));
-    MappedSet ms(pipe.pool(), 1 + M, ps);
-    int rc;
-    if ((rc = ms.reserve())) return rc;
-    if (ms.map(0, dat_fd, mapped, false)) return kFallback;
-    for (int j = 0; j < M; ++j)
-        if (ms.map(1 + j, out[K + j].fd, shard_size, true)) return kFallback;
-    clk.map = StageClock::now() - clk.t0;
-    uint8_t* dev = nullptr;
-    if ((rc = ms.register_all(&dev))) return rc;
-    clk.reg = StageClock::now() - clk.t0 - clk.map;
-    uint8_t* const dat_d = dev;
-    uint8_t* const par_d = dev + ps;
-    hipStream_t st = pipe.stream0();
-    // declared after ms, so destroyed before it: whatever the return path, the
-    // kernels have finished before the pages are unregistered and unmapped
-    const StreamDrain drain{st};
-    // GPU: every large row (encoder.rs:215-226), then the whole small rows as one batch
-    for (uint64_t r = 0; r < n_large; ++r)
-        if ((rc = run_apply(*enc, K, dat_d + r * large_row, 0, large, par_d + r * large, 0, ps, large, 1, nullptr,
-                            nullptr, st, nullptr, /*over_pcie=*/true)))
-            return rc;
-    for (uint64_t r0 = 0; r0 < full_small; r0 += (1u << 30)) {
-        const uint64_t nr = std::min<uint64_t>(full_small - r0, 1u << 30);
-        if ((rc = run_apply(*enc, K, dat_d + n_large * large_row + r0 * small_row, small_row, small,
-                            par_d + n_large * large + r0 * small, small, ps, small, uint32_t(nr), nullptr, nullptr,
-                            st, nullptr, /*over_pcie=*/true)))
-            return rc;
-    }
-    // CPU, meanwhile: the data shards are .dat blocks, written from the mapping
-    const uint8_t* dat = ms.slot(0);
-    ErrorSlot err;
-    std::vector<std::function<void()>> tasks;
-    const uint64_t rows_per_task = std::max<uint64_t>(1, (64ull << 20) / small);  // ~64 MiB per pwritev batch
-    for (int j = 0; j < K; ++j) {
-        for (uint64_t r = 0; r < n_large; ++r)
-            for (uint64_t t = 0; t < large; t += kLargeSlice * 4)
-                tasks.push_back([&, j, r, t] {
-                    const uint64_t n = std::min(kLargeSlice * 4, large - t);
-                    pwritev_all(out[j].fd, {iovec{const_cast<uint8_t*>(dat + r * large_row + j * large + t), n}},
-                                r * large + t, err);
-                });
-        for (uint64_t r0 = 0; r0 < full_small; r0 += rows_per_task)
-            tasks.push_back([&, j, r0] {
-                const uint64_t nr = std::min(rows_per_task, full_small - r0);
-                std::vector<iovec> iov;
-                for (uint64_t r = r0; r < r0 + nr; ++r)
-                    iov.push_back(iovec{const_cast<uint8_t*>(dat + n_large * large_row + r * small_row + j * small), small});
-                pwritev_all(out[j].fd, std::move(iov), n_large * large + r0 * small, err);
-            });
-    }
-    const int64_t c0 = StageClock::now();
-    pipe.pool().run_all(tasks);
-    clk.cpu = StageClock::now() - c0;
-    // the partial last row, staged (pread_zero pads it), queued behind the kernels
-    if (full_small < n_small) {
-        pipe.submit(small_rows_job(dat_fd, out, enc, mapped, n_large * large + full_small * small, 1, small,
-                                   (small_row + 255) / 256 * 256, {}));
-        if ((rc = pipe.drain())) {
-            (void)hipStreamSynchronize(st);
-            return rc;
-        }
-    }
-    const int64_t g0 = StageClock::now();
-    const hipError_t he = hipStreamSynchronize(st);
-    clk.gpu = StageClock::now() - g0;
-    if (he != hipSuccess) return hip_fail(he, "hipStreamSynchronize");
-    const int64_t u0 = StageClock::now();
-    ms.release();
-    clk.unreg = StageClock::now() - u0;
-    clk.print("encode");
-    if (err.failed()) return fail_with(err.code.load(), err.detail, err.values);
-    return HEC_OK;
-}
-
-// rebuild_ec_files' coding over the page cache: the first 10 present shard
-// files mapped read-only and the missing ones (ftruncate'd to rows * row
-// size, the bytes the reference writes) mapped writable, all at one stride,
-// so one launch decodes every row in place (the staged layout, [14][rows]).
-int rebuild_zero_copy(FilePipeline& pipe, const Fd* in, const Fd* out, const std::vector<uint32_t>& in_ids,
-                      const std::vector<uint32_t>& out_ids, uint64_t rows, uint64_t row_size, const DevicePlanSet& ps) {
-    ZcClock clk;
-    const uint64_t bytes = rows * row_size;
-    for (uint32_t id : in_ids)
-        if (!regular_file(in[id].fd)) return kFallback;
-    for (uint32_t id : out_ids)
-        if (!regular_file(out[id].fd) || ::ftruncate(out[id].fd, off_t(bytes)) != 0) return kFallback;
-    const uint64_t stride = page_round(bytes);
-    MappedSet ms(pipe.pool(), N, stride);
-    int rc;
-    if ((rc = ms.reserve())) return rc;
-    for (uint32_t id : in_ids)
-        if (ms.map(int(id), in[id].fd, bytes, false)) return kFallback;
-    for (uint32_t id : out_ids)
-        if (ms.map(int(id), out[id].fd, bytes, true)) return kFallback;
-    clk.map = StageClock::now() - clk.t0;
-    uint8_t* dev = nullptr;
-    if ((rc = ms.register_all(&dev))) return rc;
-    clk.reg = StageClock::now() - clk.t0 - clk.map;
-    hipStream_t st = pipe.stream0();
-    const StreamDrain drain{st};  // destroyed before ms: kernels done before unregistering
-    for (uint64_t r0 = 0; r0 < rows; r0 += (1u << 30)) {
-        const uint64_t nr = std::min<uint64_t>(rows - r0, 1u << 30);
-        if ((rc = run_apply(ps, K, dev + r0 * row_size, row_size, stride, dev + r0 * row_size, row_size, stride,
-                            row_size, uint32_t(nr), nullptr, nullptr, st)))
-            return rc;
-    }
-    const int64_t g0 = StageClock::now();
-    const hipError_t he = hipStreamSynchronize(st);
-    clk.gpu = StageClock::now() - g0;
-    if (he != hipSuccess) return hip_fail(he, "hipStreamSynchronize");
-    const int64_t u0 = StageClock::now();
-    ms.release();
-    clk.unreg = StageClock::now() - u0;
-    clk.print("rebuild");
-    return HEC_OK;
-}
-
 }  // namespace
 
 static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint64_t large, uint64_t small) {
@@ -852,13 +546,11 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     if (rc) return rc;
     if (buf_size == 0) return fail(HEC_ERR_INVALID_ARGUMENT, "zero buffer size");
 
-    // the zero-copy path maps the parity files shared and writable
-    const bool zero_copy = file_zero_copy_mode().load() != 0 && st.st_size > 0;
     Fd out[N];  // open_ec_files(base, false): create + truncate (encoder.rs:111-127)
     {
         bool all[N];
         std::fill(all, all + N, true);
-        if ((rc = open_outputs(base, all, out, zero_copy ? O_RDWR : O_WRONLY))) return rc;
+        if ((rc = open_outputs(base, all, out))) return rc;
     }
     const uint64_t large_row = large * K, small_row = small * K;
     // the reference checks block % buf at the first row of each kind (encoder.rs:139-144)
@@ -873,23 +565,6 @@ static int write_ec_files_impl(const std::string& base, uint64_t buf_size, uint6
     const uint64_t n_small = small_bytes > 0 ? (uint64_t(small_bytes) + small_row - 1) / small_row : 0;
     GeomDevice* gd;
     if ((rc = geom_device(rs.rs, &gd))) return rc;
-    // zero copy, unless the small rows' block-size check fails (the reference
-    // writes the large rows, then returns UnexpectedBlockSize: the staged path
-    // below reproduces that order)
-    if (zero_copy && !(n_small > 0 && small % buf_size != 0)) {
-        PipelineLease lease;  // the tail row's staging: one small row
-        if ((rc = lease_pipeline((small_row + 255) / 256 * 256 + std::max<uint64_t>(256, small * M),
-                                 (small_row + 255) / 256 * 256 + std::max<uint64_t>(256, small * M), lease)))
-            return rc;
-        rc = write_zero_copy(*lease.pipe, dat.fd, uint64_t(remaining), out, &gd->encode, large, small, n_large, n_small);
-        if (rc != kFallback && rc != kNoRows) {
-            ++g_zc_calls;
-            return rc;
-        }
-        if (rc == kFallback) ++g_zc_fallbacks;
-        // file pages refused by the runtime: the staged pipeline (outputs are
-        // rewritten in full, so the sizes set above are harmless)
-    }
     std::shared_future<void> prealloc;
     {
         int fds[N];
@@ -955,7 +630,6 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
     bool has[N];
     Fd in[N], out[N];
     std::vector<uint32_t> rebuilt;
-    const bool zero_copy = file_zero_copy_mode().load() != 0;  // outputs mapped writable
     for (int i = 0; i < N; ++i) {
         const std::string name = shard_name(base, i);
         struct stat st;
@@ -966,7 +640,7 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
         } else {
             if (errno != ENOENT) return fail_errno(HEC_ERR_IO, "stat " + name, errno);
             has[i] = false;
-            out[i].fd = ::open(name.c_str(), (zero_copy ? O_RDWR : O_WRONLY) | O_CREAT | O_TRUNC, 0644);
+            out[i].fd = ::open(name.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
             if (out[i].fd < 0) return fail_errno(HEC_ERR_IO, "open " + name, errno);
             rebuilt.push_back(uint32_t(i));
         }
@@ -1037,53 +711,38 @@ static int rebuild_ec_files_impl(const std::string& base, uint32_t* ids, size_t*
             ~PsGuard() { p.release(); }
         } pg{ps};
         if ((rc = ps.upload(hp, nullptr, nullptr))) return rc;
-        bool done = false;
-        if (zero_copy) {
-            PipelineLease lease;  // its I/O pool and stream
-            if ((rc = lease_pipeline(256, 256, lease))) return rc;
-            rc = rebuild_zero_copy(*lease.pipe, in, out, in_ids, out_ids, rows, row_size, ps);
-            if (rc != kFallback) {
-                ++g_zc_calls;
-                if (rc) return rc;
-                done = true;
-            } else {
-                ++g_zc_fallbacks;
-            }
+        std::shared_future<void> prealloc;
+        {
+            int fds[N];
+            for (int i = 0; i < N; ++i) fds[i] = has[i] ? -1 : out[i].fd;
+            prealloc = preallocate_async(fds, N, rows * row_size);
         }
-        if (!done) {
-            std::shared_future<void> prealloc;
-            {
-                int fds[N];
-                for (int i = 0; i < N; ++i) fds[i] = has[i] ? -1 : out[i].fd;
-                prealloc = preallocate_async(fds, N, rows * row_size);
+        const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(rows, kBatchBytes / (K * row_size)));
+        const uint64_t slot = B * row_size;  // bytes per shard slot: layout [14][B rows]
+        PipelineLease lease;
+        if ((rc = lease_pipeline(slot * N, slot * N, lease))) return rc;
+        FilePipeline& pipe = *lease.pipe;
+        const DevicePlanSet* psp = &ps;
+        for (uint64_t r0 = 0; r0 < rows && !pipe.errors().failed(); r0 += B) {
+            const uint64_t nr = std::min(B, rows - r0);
+            const uint64_t off = r0 * row_size;
+            Job job;
+            for (uint32_t id : in_ids) {
+                add_reads(job.reads, in[id].fd, id * slot, nr * row_size, off, row_size, 1);
+                job.h2d.push_back({id * slot, id * slot, nr * row_size});
             }
-            const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(rows, kBatchBytes / (K * row_size)));
-            const uint64_t slot = B * row_size;  // bytes per shard slot: layout [14][B rows]
-            PipelineLease lease;
-            if ((rc = lease_pipeline(slot * N, slot * N, lease))) return rc;
-            FilePipeline& pipe = *lease.pipe;
-            const DevicePlanSet* psp = &ps;
-            for (uint64_t r0 = 0; r0 < rows && !pipe.errors().failed(); r0 += B) {
-                const uint64_t nr = std::min(B, rows - r0);
-                const uint64_t off = r0 * row_size;
-                Job job;
-                for (uint32_t id : in_ids) {
-                    add_reads(job.reads, in[id].fd, id * slot, nr * row_size, off, row_size, 1);
-                    job.h2d.push_back({id * slot, id * slot, nr * row_size});
-                }
-                job.kernel = [=](uint8_t* d, hipStream_t s) {
-                    return run_apply(*psp, K, d, row_size, slot, d, row_size, slot, row_size, uint32_t(nr), nullptr,
-                                     nullptr, s);
-                };
-                for (uint32_t id : out_ids) {
-                    job.d2h.push_back({id * slot, id * slot, nr * row_size});
-                    job.writes.push_back({out[id].fd, off, {{id * slot, nr * row_size}}});
-                }
-                job.write_gate = prealloc;
-                pipe.submit(std::move(job));
+            job.kernel = [=](uint8_t* d, hipStream_t s) {
+                return run_apply(*psp, K, d, row_size, slot, d, row_size, slot, row_size, uint32_t(nr), nullptr,
+                                 nullptr, s);
+            };
+            for (uint32_t id : out_ids) {
+                job.d2h.push_back({id * slot, id * slot, nr * row_size});
+                job.writes.push_back({out[id].fd, off, {{id * slot, nr * row_size}}});
             }
-            if ((rc = pipe.drain())) return rc;
+            job.write_gate = prealloc;
+            pipe.submit(std::move(job));
         }
+        if ((rc = pipe.drain())) return rc;
     }
     if (end_rc != HEC_OK) return fail_values(end_rc, end_detail, end_expected, end_actual);
     if (n_ids) *n_ids = rebuilt.size();
@@ -1106,17 +765,6 @@ int hec_write_ec_files_ex(const char* base_filename, uint64_t buf_size, uint64_t
 int hec_write_ec_files(const char* base_filename) {
     // write_ec_files: buf 256 KiB, large 1 GiB, small 1 MiB (encoder.rs:39-46)
     return hec_write_ec_files_ex(base_filename, 256 * 1024, HEC_LARGE_BLOCK_SIZE, HEC_SMALL_BLOCK_SIZE);
-}
-
-int hec_set_file_zero_copy(int on) {
-    hec::file_zero_copy_mode() = on != 0 ? 1 : 0;
-    return HEC_OK;
-}
-
-int hec_file_path_stats(uint64_t* zero_copy_calls, uint64_t* fallbacks) {
-    if (zero_copy_calls) *zero_copy_calls = hec::g_zc_calls.load();
-    if (fallbacks) *fallbacks = hec::g_zc_fallbacks.load();
-    return HEC_OK;
 }
 
 int hec_rebuild_ec_files(const char* base_filename, uint32_t* rebuilt_ids, size_t* n_rebuilt) {

@@ -180,7 +180,7 @@ void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>&
     for (size_t i = 0; i < n; ++i) fn(i);  // every pool of this device busy: this thread alone
 }
 
-// Process-wide launch knobs (measurement switches, speed only): set under a
+// Process-wide launch knobs (hec_set_decode_vector_bytes; speed only): set under a
 // mutex, read as a snapshot per launch, so concurrent callers never see a
 // half-updated configuration.
 namespace {
@@ -431,10 +431,7 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
 // on two boxes, ahead in each of the 7 rounds (profiles/r04/e2e_encode_kernels_*.jsonl, profiles/r04/INDEX.md).
 LaunchConfig pcie_encode_config(const LaunchConfig& cfg) {
     LaunchConfig c = cfg;
-    if (c.pcie_enc_narrow && c.mode == 0) {
-        c.bitslice = 0;
-        c.enc_vec_bytes = 8;
-    }
+    c.over_pcie = true;
     return c;
 }
 
@@ -763,76 +760,15 @@ int hec_get_device(int* device) {
 const char* hec_encode_kernel_name(uint64_t shard_len) { return encode_kernel_name(shard_len, launch_config()); }
 const char* hec_decode_kernel_name(uint64_t shard_len) { return decode_kernel_name(shard_len, launch_config()); }
 
-int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, int blocks_per_cu) {
-    if (vec_per_thread != 1 && vec_per_thread != 2 && vec_per_thread != 4)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "vec_per_thread must be 1, 2 or 4");
-    if (blocks_per_cu < 0 || blocks_per_cu > 8) return fail(HEC_ERR_INVALID_ARGUMENT, "blocks_per_cu in 0..8");
-    if (xcd_remap < 0) return fail(HEC_ERR_INVALID_ARGUMENT, "xcd_remap >= 0");
-    update_launch_config([&](LaunchConfig& c) {
-        c.vec_per_thread = vec_per_thread;
-        c.max_blocks = max_blocks < 0 ? 0 : max_blocks;
-        c.xcd_remap = xcd_remap;
-        c.blocks_per_cu = blocks_per_cu;
-    });
-    return HEC_OK;
-}
-
-int hec_set_xcd_parts(int parts) {
-    if (parts < 1 || parts > 1024) return fail(HEC_ERR_INVALID_ARGUMENT, "parts in 1..1024");
-    update_launch_config([&](LaunchConfig& c) { c.xcd_parts = parts; });
-    return HEC_OK;
-}
-
-int hec_set_chunk_rotation(int on) {
-    update_launch_config([&](LaunchConfig& c) { c.chunk_rot = on ? 1 : 0; });
-    return HEC_OK;
-}
-
-int hec_set_workgroup_size(int threads) {
-    if (threads != 128 && threads != 256 && threads != 512 && threads != 1024)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "workgroup size must be 128, 256, 512 or 1024");
-    update_launch_config([&](LaunchConfig& c) { c.wg_threads = threads; });
-    return HEC_OK;
-}
-
 int hec_set_decode_vector_bytes(int bytes) {
-    if (bytes != 4 && bytes != 8 && bytes != 16)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "decode vector bytes must be 4, 8 or 16");
+    if (bytes != 8 && bytes != 16 && bytes != 32)
+        return fail(HEC_ERR_INVALID_ARGUMENT, "decode vector bytes must be 8, 16 or 32");
     update_launch_config([&](LaunchConfig& c) { c.dec_vec_bytes = bytes; });
-    return HEC_OK;
-}
-
-int hec_set_encode_vector_bytes(int bytes) {
-    if (bytes != 4 && bytes != 8 && bytes != 16)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "encode vector bytes must be 4, 8 or 16");
-    update_launch_config([&](LaunchConfig& c) { c.enc_vec_bytes = bytes; });
-    return HEC_OK;
-}
-
-int hec_set_bitslice_vector_bytes(int bytes) {
-    if (bytes != 8 && bytes != 16) return fail(HEC_ERR_INVALID_ARGUMENT, "bit-sliced vector bytes must be 8 or 16");
-    update_launch_config([&](LaunchConfig& c) { c.bs_vec_bytes = bytes; });
-    return HEC_OK;
-}
-
-int hec_set_encode_kernel(int kind) {
-    if (kind != 0 && kind != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "encode kernel must be 0 or 1");
-    update_launch_config([&](LaunchConfig& c) { c.bitslice = kind; });
-    return HEC_OK;
-}
-
-int hec_set_host_encode_narrow(int on) {
-    update_launch_config([&](LaunchConfig& c) { c.pcie_enc_narrow = on ? 1 : 0; });
     return HEC_OK;
 }
 
 const char* hec_host_encode_kernel_name(uint64_t shard_len) {
     return encode_kernel_name(shard_len, pcie_encode_config(launch_config()));
-}
-
-int hec_set_ragged_encode_remap(int on) {
-    update_launch_config([&](LaunchConfig& c) { c.ragged_encode_remap = on ? 1 : 0; });
-    return HEC_OK;
 }
 
 int hec_set_host_staging(uint64_t max_bytes) {
@@ -842,12 +778,6 @@ int hec_set_host_staging(uint64_t max_bytes) {
 
 int hec_set_completion_signal(uint64_t max_bytes) {
     completion_flag_max() = max_bytes;
-    return HEC_OK;
-}
-
-int hec_set_kernel_mode(int mode) {
-    if (mode != 0 && mode != 1) return fail(HEC_ERR_INVALID_ARGUMENT, "mode must be 0 or 1");
-    update_launch_config([&](LaunchConfig& c) { c.mode = mode; });
     return HEC_OK;
 }
 

@@ -170,7 +170,8 @@ hipError_t copy2d(void* dst, uint64_t dpitch, const void* src, uint64_t spitch, 
 // for the copy pipeline (profiles/r02/HISTORY.md "host path"). The whole
 // [p, p + span) must be one registered host range; anything else (pageable
 // memory, device memory, a range running past the allocation) takes the copy
-// pipeline. hec_set_host_zero_copy(0) disables it (measurement).
+// pipeline. hec_set_host_zero_copy(0) disables it (the CUs then stay free
+// while SDMA engines move the bytes).
 bool host_device_view(const void* p, uint64_t span, uint8_t** dev) {
     if (!zero_copy_enabled() || span == 0) return false;
     hipPointerAttribute_t a{}, b{};

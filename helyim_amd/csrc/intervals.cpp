@@ -207,7 +207,6 @@ int compact_reconstruct_104(const hec_rs* rs, const std::vector<CompactJob>& job
     ra.tabs = gd->decode_dense.tabs;
     ra.lut = gd->decode_dense.lut;
     ra.compact = 1;
-    ra.xcd_remap = launch_config().xcd_remap == 1 ? 1u : 0u;
     if (items.size() == 1) {  // one stripe (a per-call reconstruct): descriptor as a kernel argument
         ra.inline_one = 1;
         ra.one = items[0];
@@ -324,34 +323,24 @@ uint64_t ragged_chunks(const hec_stripe_desc& d, bool decode, uint32_t chunk_byt
     return (uint64_t(d.shard_len) + chunk_bytes - 1) / chunk_bytes;
 }
 
-// The kernel and workgroup order of one ragged launch, shared by gpu_ragged
-// and hec_ragged_kernel_name so a reported name is the kernel that runs.
+// The kernel of one ragged launch, shared by gpu_ragged and
+// hec_ragged_kernel_name so a reported name is the kernel that runs. Both
+// ragged kernels deal each XCD a contiguous eighth of the launch's column
+// ranges (ragged_block, rs_kernels.hip).
 struct RaggedPick {
     bool bitslice;  // encode with every length a multiple of 8 KiB: rs104_bs_ragged_kernel
-    bool remap;     // XCD eighths (else dispatch order)
 };
-RaggedPick ragged_pick(const hec_stripe_desc* descs, uint32_t n, bool decode, const LaunchConfig& cfg) {
+RaggedPick ragged_pick(const hec_stripe_desc* descs, uint32_t n, bool decode) {
     RaggedPick p;
-    p.bitslice = !decode && cfg.bitslice != 0 && cfg.mode == 0;
+    p.bitslice = !decode;
     for (uint32_t j = 0; j < n && p.bitslice; ++j) p.bitslice = descs[j].shard_len % kBsChunk == 0;
-    // XCD eighths: the ragged decode +2% on the bench batch (with the no-op
-    // skip +10% on the mixed workload, profiles/r02/ab_ragged_remap_skip.jsonl);
-    // the bit-sliced ragged encode +2% at 512 mixed stripes, +7% at 4096 and
-    // +9% on uniform 4 MiB stripes (profiles/r03/sweep_mixed2.jsonl). The
-    // global knob (hec_set_launch_config xcd_remap 0) turns both off.
-    p.remap = cfg.xcd_remap == 1 && (decode || cfg.ragged_encode_remap != 0);
     return p;
 }
 
 const char* ragged_name(const RaggedPick& p, bool decode) {
-    if (decode)
-        return p.remap ? "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
-                       : "rs104_ragged_kernel<DEC=true> (table lookup, dispatch order)";
-    if (p.bitslice)
-        return p.remap ? "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
-                       : "rs104_bs_ragged_kernel (bit-sliced, dispatch order)";
-    return p.remap ? "rs104_ragged_kernel<DEC=false> (table lookup, XCD eighths)"
-                   : "rs104_ragged_kernel<DEC=false> (table lookup, dispatch order)";
+    if (decode) return "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)";
+    if (p.bitslice) return "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)";
+    return "rs104_ragged_kernel<DEC=false> (table lookup, XCD eighths)";
 }
 
 // Device-resident ragged batches: stripe descriptors come from the host, data
@@ -362,8 +351,7 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     if (!rs || !d_base || (n && !descs)) return fail(HEC_ERR_INVALID_ARGUMENT, "null argument");
     if (!(rs->k == 10 && rs->m == 4))
         return fail(HEC_ERR_INVALID_ARGUMENT, "ragged device batches are RS(10,4) only");
-    const LaunchConfig cfg = launch_config();
-    const RaggedPick pick = ragged_pick(descs, n, decode, cfg);
+    const RaggedPick pick = ragged_pick(descs, n, decode);
     const bool bitslice = pick.bitslice;
     const uint32_t chunk_bytes = bitslice ? kBsChunk : 4096;
     uint64_t n_blocks = 0;
@@ -411,7 +399,6 @@ int gpu_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_stripe_desc* descs
     ra.tabs = decode ? gd->decode_dense.tabs : gd->encode.tabs;
     ra.lut = decode ? gd->decode_dense.lut : nullptr;
     ra.bad_count = d_bad;
-    ra.xcd_remap = pick.remap ? 1u : 0u;
     if (n_blocks == 0) {  // every stripe already complete (upstream no-op)
         HEC_HIP(hipEventRecord(slot.free, stream));
         return HEC_OK;
@@ -441,7 +428,7 @@ int hec_gpu_reconstruct_ragged(const hec_rs_t* rs, uint8_t* d_base, const hec_st
 
 const char* hec_ragged_kernel_name(const hec_stripe_desc* descs, uint32_t n_stripes, int decode) {
     if (n_stripes && !descs) return "invalid argument";
-    return hec::ragged_name(hec::ragged_pick(descs, n_stripes, decode != 0, hec::launch_config()), decode != 0);
+    return hec::ragged_name(hec::ragged_pick(descs, n_stripes, decode != 0), decode != 0);
 }
 
 }  // extern "C"

@@ -12,11 +12,23 @@
 //    of the CPU's 10 read-modify-write sweeps per output.
 //  * GF(2^8) constant multiply as a byte-sliced SWAR lookup on whole dwords:
 //    c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6]; each table is <= 8 bytes, so one
-//    v_perm_b32 performs four lookups. Three v_perm + one v_bitop3 (xor3) + one
-//    xor per coefficient per dword; selectors are shared by all output rows.
+//    v_perm_b32 performs four lookups. Three v_perm + 1.5 v_bitop3 (xor3) per
+//    coefficient per dword; selectors are shared by all output rows.
 //  * Tables and shard ids are wave-uniform -> scalar loads (SGPRs); only the
-//    data is vector traffic: coalesced 16 B/lane loads and stores (1 KiB per
-//    wave instruction), non-temporal since every byte is touched once.
+//    data is vector traffic: coalesced loads and stores (1 KiB per wave
+//    instruction at 16 B per lane), non-temporal since every byte is touched
+//    once.
+//  * The encode of shard lengths that are a multiple of 8 KiB is bit-sliced
+//    (rs104_bs_encode_kernel): the fixed parity matrix as a generated XOR
+//    program over bit planes, half the table multiply's VALU work.
+//
+// Every kernel here is a product path (rs104_pick / ragged_pick choose among
+// them by shard length and alignment), except rs104_wide_kernel, the round-6
+// decode experiment selected only by hec_set_decode_vector_bytes(32).
+// Variants measured and not kept (XOR-only twins, the pair kernel, chunk
+// rotation, 128/512/1024-thread launches, 4 B and 8 B-load variants,
+// occupancy caps) are in git history and profiles/r0*/INDEX.md; the math-free
+// stream ceilings live in tools/membench.hip.
 #include <algorithm>
 #include <type_traits>
 
@@ -26,6 +38,7 @@
 namespace hec {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Scalar-cache view of plan metadata: uniform loads through the constant
 // address space become s_load (SGPR) instead of per-lane vector loads.
@@ -33,19 +46,18 @@ template <typename T>
 __device__ __forceinline__ const __attribute__((address_space(4))) T* as_const(const T* p) {
     return (const __attribute__((address_space(4))) T*)(p);
 }
+typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
 // Cache policy of the streamed shard bytes (each is touched exactly once).
-// Build-time switches for measurement variants (tools/tune.py).
+// Build-time switches for measurement variants (Makefile VARIANTS).
 #ifndef HEC_NT_LOAD
 #define HEC_NT_LOAD 1
 #endif
 #ifndef HEC_NT_STORE
 #define HEC_NT_STORE 1
 #endif
-// Bit-sliced decode: 1 = the selected parity rows are loaded with the data
-// (in flight during the XOR program, more VGPRs); 0 = after the program.
-// Table kernels: 1 = all ten shard loads issued before the math (the
-// shipped form; 0 = the scheduler's interleaving, a measurement variant).
+// Table kernels: 1 = all ten shard loads issued before the math (the shipped
+// form); 0 = the scheduler's interleaving (measurement variant `lf0`).
 #ifndef HEC_LOADS_FIRST
 #define HEC_LOADS_FIRST 1
 #endif
@@ -55,6 +67,8 @@ __device__ __forceinline__ const __attribute__((address_space(4))) T* as_const(c
 // streamed shards are accessed through address_space(1) pointers to get `nt`.
 typedef const __attribute__((address_space(1))) u32x4* gcu32x4p;
 typedef __attribute__((address_space(1))) u32x4* gu32x4p;
+typedef const __attribute__((address_space(1))) uint8_t* gcu8p;
+typedef __attribute__((address_space(1))) uint8_t* gu8p;
 
 __device__ __forceinline__ u32x4 load_full(const uint8_t* p, bool aligned) {
     if (aligned) {
@@ -84,8 +98,6 @@ __device__ __forceinline__ void store_full(uint8_t* p, u32x4 v, bool aligned) {
 // Streamed access at (uniform shard base) + (lane offset): the base is moved
 // to the global address space before the offset is added, so a 32-bit offset
 // becomes the saddr form (SGPR base + VGPR offset) with no 64-bit VALU math.
-typedef const __attribute__((address_space(1))) uint8_t* gcu8p;
-typedef __attribute__((address_space(1))) uint8_t* gu8p;
 // Measurement variants (Makefile VARIANTS): HEC_LOAD_CPOL / HEC_STORE_CPOL >= 0
 // route 32-bit-offset accesses through raw buffer instructions with that
 // cache-policy word (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
@@ -138,7 +150,7 @@ __device__ __noinline__ void store_tail(uint8_t* p, u32x4 v, uint64_t avail) {
 
 // acc[r] ^= coef(r) * d for R output rows; tab -> [rows][5] words of this input.
 template <int R>
-__device__ __forceinline__ void gf_mac(u32x4 (&acc)[R], const u32x4 d, const __attribute__((address_space(4))) uint32_t* tab) {
+__device__ __forceinline__ void gf_mac(u32x4 (&acc)[R], const u32x4 d, cu32p tab) {
     uint32_t s0[4], s1[4], s2[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -161,8 +173,6 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R], const u32x4 d, const __a
         }
     }
 }
-
-typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
 // Two inputs at once: the six lookups of a row are folded into the
 // accumulator by three 3-input XORs (v_bitop3) instead of four ops.
@@ -218,59 +228,41 @@ __device__ __forceinline__ void gf_mac2(V (&acc)[R], const V d0, const V d1, cu3
     }
 }
 
-// Diagnostic bandwidth ceiling: same loads/stores/addressing, GF math replaced
-// by a plain XOR (wrong parity by design; never used by the product paths).
-template <int R, bool XORONLY>
-__device__ __forceinline__ void mac(u32x4 (&acc)[R], const u32x4 d, cu32p tab) {
-    if constexpr (XORONLY) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] ^= d;
-    } else {
-        gf_mac<R>(acc, d, tab);
-    }
-}
-
-// One group of R (<= 4) output rows of a plan over U vectors per lane.
+// One group of R (<= 4) output rows of a plan, one 16-byte vector per lane.
 // K > 0: compile-time input count (all K loads issued before any math);
-// K == 0: runtime nin loop. Lanes whose 16-byte vector crosses the end of the
-// shard take the byte-wise tail path (only in the last chunk of a stripe).
-template <int K, int R, int U, bool ALIGNED, bool XORONLY = false>
+// K == 0: runtime nin loop. Lanes whose vector crosses the end of the shard
+// take the byte-wise tail path (only in the last chunk of a stripe).
+template <int K, int R, bool ALIGNED>
 __device__ __forceinline__ void apply_group(const ApplyArgs& a, const uint8_t* in_b, uint8_t* out_b,
                                             cu32p in_ids, cu32p out_ids, cu32p tab, uint32_t nin,
                                             uint32_t tab_row_stride, uint64_t chunk_off) {
+    const uint64_t o = chunk_off + threadIdx.x * kVecBytes;
+    if (o >= a.len) return;
+    const uint64_t avail = a.len - o;
+    u32x4 acc[R];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t o = chunk_off + uint64_t(u) * (kThreads * kVecBytes) + threadIdx.x * kVecBytes;
-        if (o >= a.len) break;
-        const uint64_t avail = a.len - o;
-        u32x4 acc[R];
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+    if (avail >= kVecBytes) {
+        if constexpr (K > 0) {
+            u32x4 d[K];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-        if (avail >= kVecBytes) {
-            if constexpr (K > 0) {
-                u32x4 d[K];
+            for (int i = 0; i < K; ++i) d[i] = load_full(in_b + uint64_t(in_ids[i]) * a.in_shard + o, ALIGNED);
 #pragma unroll
-                for (int i = 0; i < K; ++i)
-                    d[i] = load_full(in_b + uint64_t(in_ids[i]) * a.in_shard + o, ALIGNED);
-#pragma unroll
-                for (int i = 0; i < K; ++i) mac<R, XORONLY>(acc, d[i], tab + i * tab_row_stride);
-            } else {
-                for (uint32_t i = 0; i < nin; ++i) {
-                    const u32x4 d = load_full(in_b + uint64_t(in_ids[i]) * a.in_shard + o, ALIGNED);
-                    gf_mac<R>(acc, d, tab + i * tab_row_stride);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                store_full(out_b + uint64_t(out_ids[r]) * a.out_shard + o, acc[r], ALIGNED);
+            for (int i = 0; i < K; ++i) gf_mac<R>(acc, d[i], tab + i * tab_row_stride);
         } else {
             for (uint32_t i = 0; i < nin; ++i) {
-                const u32x4 d = load_tail(in_b + uint64_t(in_ids[i]) * a.in_shard + o, avail);
+                const u32x4 d = load_full(in_b + uint64_t(in_ids[i]) * a.in_shard + o, ALIGNED);
                 gf_mac<R>(acc, d, tab + i * tab_row_stride);
             }
-            for (int r = 0; r < R; ++r)
-                store_tail(out_b + uint64_t(out_ids[r]) * a.out_shard + o, acc[r], avail);
         }
+#pragma unroll
+        for (int r = 0; r < R; ++r) store_full(out_b + uint64_t(out_ids[r]) * a.out_shard + o, acc[r], ALIGNED);
+    } else {
+        for (uint32_t i = 0; i < nin; ++i) {
+            const u32x4 d = load_tail(in_b + uint64_t(in_ids[i]) * a.in_shard + o, avail);
+            gf_mac<R>(acc, d, tab + i * tab_row_stride);
+        }
+        for (int r = 0; r < R; ++r) store_tail(out_b + uint64_t(out_ids[r]) * a.out_shard + o, acc[r], avail);
     }
 }
 
@@ -294,16 +286,15 @@ __device__ __forceinline__ void signal_done(uint32_t* count, uint32_t* flag, uin
     }
 }
 
-template <int K, int U, bool ALIGNED, bool XORONLY = false>
+// Generic plan interpreter (any k + m <= 256, unaligned bases and strides,
+// ad-hoc host plans): grid-stride over (stripe, 4 KiB chunk) items.
+template <int K, bool ALIGNED>
 __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
     // XCD-aware chunk mapping: workgroups b, b+8, b+16, ... are dealt to one
     // XCD (MI355X_MICROARCH.md, dispatch), so a bijective remap hands them
     // consecutive chunks. Speed only: correctness never depends on placement.
-    uint64_t first = blockIdx.x;
-    if (a.xcd_remap) {
-        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blockIdx.x % 8;
-        first = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
-    }
+    const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blockIdx.x % 8;
+    const uint64_t first = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
     for (uint64_t item = first; item < a.n_items; item += gridDim.x) {
         const uint32_t stripe = uint32_t(item / a.chunks_per_stripe);
         const uint32_t chunk = uint32_t(item - uint64_t(stripe) * a.chunks_per_stripe);
@@ -324,15 +315,15 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
         cu32p out_ids = in_ids + p.nin;
         cu32p tab = as_const(a.tabs) + p.tab_off;
         const uint32_t row_stride = p.tab_rows * 5;  // words per input
-        const uint64_t chunk_off = uint64_t(chunk) * (uint64_t(U) * kThreads * kVecBytes);
+        const uint64_t chunk_off = uint64_t(chunk) * (kThreads * kVecBytes);
         for (uint32_t g = 0; g < p.nout; g += 4) {
             const uint32_t R = p.nout - g < 4 ? p.nout - g : 4;
             cu32p tg = tab + g * 5;
             switch (R) {
-                case 4: apply_group<K, 4, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
-                case 3: apply_group<K, 3, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
-                case 2: apply_group<K, 2, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
-                default: apply_group<K, 1, U, ALIGNED, XORONLY>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                case 4: apply_group<K, 4, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                case 3: apply_group<K, 3, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                case 2: apply_group<K, 2, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
+                default: apply_group<K, 1, ALIGNED>(a, in_b, out_b, in_ids, out_ids + g, tg, p.nin, row_stride, chunk_off); break;
             }
         }
     }
@@ -342,88 +333,41 @@ __global__ __launch_bounds__(kThreads) void rs_apply_kernel(ApplyArgs a) {
 // ---------------------------------------------------------------------------
 // RS(10,4) fast paths (k = 10, n = 14, 16-byte aligned strides): the shard ids
 // come from kernel arguments (encode) or straight from the stripe's present
-// mask with scalar bit scans (decode), so a workgroup issues its ten 16-byte
-// loads after at most ONE scalar load; the coefficient tables (fixed stride
-// of 4 rows x 5 words per input) arrive in parallel with the data.
+// mask with scalar bit scans (decode), so a workgroup issues its ten loads
+// after at most ONE scalar load; the coefficient tables (fixed stride of 4
+// rows x 5 words per input) arrive in parallel with the data.
 // ---------------------------------------------------------------------------
-// Workgroup -> chunk mapping. Workgroups b, b+8, b+16, ... are dealt to one
-// XCD (observed round-robin dispatch; MI355X_MICROARCH.md), so:
-//   mode 0: identity;
-//   mode 1: XCD x takes the contiguous x-th eighth of all chunks;
-//   mode G >= 2: XCD x takes runs of G consecutive chunks, XCDs interleaved
-//               run by run (applied to the largest prefix divisible by 8G).
-// Always a bijection; speed only, never correctness.
-__device__ __forceinline__ uint32_t remap_block(uint32_t b, uint32_t nb, uint32_t mode, uint32_t parts = 1) {
-    if (mode == 0) return b;
-    const uint32_t x = b % 8, j = b / 8;
-    if (mode == 1 && parts > 1 && nb % (8 * parts) == 0) {
-        // XCD x spreads its workgroups over `parts` regions of the batch:
-        // region x*parts + j%parts, position j/parts within it.
-        const uint32_t q = nb / (8 * parts);
-        return (x * parts + j % parts) * q + j / parts;
-    }
-    if (mode == 1) {
-        const uint32_t q = nb / 8, r = nb % 8;
-        return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
-    }
-    const uint32_t full = nb / (8 * mode) * (8 * mode);
-    if (b >= full) return b;
-    return (j / mode) * (8 * mode) + x * mode + (j % mode);
-}
-
-// Workgroup -> (stripe, chunk) of the RS(10,4) fast paths.
-// FAST: the shipped mapping (XCD eighths, or identity) from the launcher's
-// constants (map_q8 / map_r8, FastDiv of the chunks per stripe): a handful of
-// scalar ops from blockIdx, no division, so a workgroup reaches its stripe's
-// mask load (decode) or its first data load (encode) a few cycles after
-// launch. Before, remap_block's and the stripe's runtime divisions were
-// expanded into ~100 VALU instructions and three dependent kernel-argument
-// loads sat in front of the mask load.
-// !FAST: every measurement mapping (runs of G chunks, regions per XCD,
-// hashed per-stripe rotation) through remap_block's divisions.
-template <bool FAST>
+// Workgroup -> (stripe, chunk). Workgroups b, b+8, b+16, ... are dealt to one
+// XCD (observed round-robin dispatch; MI355X_MICROARCH.md), so XCD x = b % 8
+// takes the contiguous x-th eighth of all chunks (+5-9% over dispatch order):
+// item = x*q + min(x, r) + b/8 from the launcher's constants (map_q8 / map_r8),
+// then the chunks per stripe as a multiply-shift divisor (FastDiv): a handful
+// of scalar ops from blockIdx, no division, so a workgroup reaches its
+// stripe's mask load (decode) or its first data load (encode) a few cycles
+// after launch. A bijection: speed only, never correctness.
 __device__ __forceinline__ void fast_item(const ApplyArgs& a, uint32_t per_stripe, uint32_t& stripe,
                                           uint32_t& chunk) {
-    const uint32_t b = blockIdx.x;
-    uint32_t item = b;
-    if constexpr (FAST) {
-        // Every kernel argument the workgroup will need, in SGPRs at entry:
-        // one round trip, instead of loads the compiler sinks behind the
-        // remap branch and the decode's mask checks (each a further trip).
-        asm volatile("" ::"s"(a.in_base), "s"(a.in_stripe), "s"(a.in_shard), "s"(a.out_base), "s"(a.out_stripe),
-                     "s"(a.out_shard), "s"(a.len), "s"(a.masks), "s"(a.lut), "s"(a.tabs), "s"(a.xcd_remap),
-                     "s"(a.map_q8), "s"(a.map_r8), "s"(a.cps_mul), "s"(a.cps_shift), "s"(a.chunks_per_stripe),
-                     "s"(a.chunk_rot));
-        if (a.xcd_remap) {  // XCD x = b % 8 takes the x-th eighth: x*q + min(x, r) + b/8
-            const uint32_t x = b & 7u, q = a.map_q8, r = a.map_r8;
-            item = x * q + (x < r ? x : r) + (b >> 3);
-        }
-        stripe = fastdiv(item, a.cps_mul, a.cps_shift);
-        chunk = item - stripe * per_stripe;
-        if (a.chunk_rot) {  // the !FAST rotation, modulo by the same multiply-shift
-            const uint32_t h = (stripe * 0x9E3779B1u) >> 8;
-            chunk += h - fastdiv(h, a.cps_mul, a.cps_shift) * per_stripe;
-            if (chunk >= per_stripe) chunk -= per_stripe;
-        }
-    } else {
-        item = remap_block(b, gridDim.x, a.xcd_remap, a.xcd_parts);
-        stripe = item / per_stripe;
-        chunk = item - stripe * per_stripe;
-        if (a.chunk_rot) {  // per-stripe hashed rotation of the chunk order (bijective per stripe)
-            chunk += (stripe * 0x9E3779B1u) >> 8;
-            chunk %= per_stripe;
-        }
-    }
+    // Every kernel argument the workgroup will need, in SGPRs at entry: one
+    // round trip, instead of loads the compiler sinks behind the decode's
+    // mask checks (each a further trip).
+    asm volatile("" ::"s"(a.in_base), "s"(a.in_stripe), "s"(a.in_shard), "s"(a.out_base), "s"(a.out_stripe),
+                 "s"(a.out_shard), "s"(a.len), "s"(a.masks), "s"(a.lut), "s"(a.tabs), "s"(a.map_q8),
+                 "s"(a.map_r8), "s"(a.cps_mul), "s"(a.cps_shift), "s"(a.chunks_per_stripe));
+    const uint32_t b = blockIdx.x, x = b & 7u, q = a.map_q8, r = a.map_r8;
+    const uint32_t item = x * q + (x < r ? x : r) + (b >> 3);
+    stripe = fastdiv(item, a.cps_mul, a.cps_shift);
+    chunk = item - stripe * per_stripe;
 }
 
 // One 4 KiB chunk of one RS(10,4) stripe. Encode (DEC=false): inputs 0..9 at
-// in_b, outputs 0..3 at out_b. Decode (DEC=true): in place at in_b == out_b,
+// in_b, outputs 0..3 at out_b. Decode (DEC=true): in place at in_b == out_b
+// (or COMPACT: inputs are slots 0..9 at in_b, outputs slots 0..e-1 at out_b),
 // shard ids from the present mask, tables at lut[mask] * 200 words.
 // OffT: type of the lane's byte offset in the shard. uint32_t (every ragged
 // stripe, and strided batches of shards below 4 GiB) lets each load address
 // be a scalar shard base plus a 32-bit lane offset (global_load saddr form:
 // no per-load 64-bit VALU address math).
-template <bool DEC, bool XORONLY, bool COMPACT = false, int TB = kThreads, typename OffT = uint64_t>
+template <bool DEC, bool COMPACT = false, typename OffT = uint64_t>
 __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
                                             uint64_t out_shard, uint64_t len, uint32_t chunk, uint32_t mask_in,
                                             cu32p tab, cu32p lut, uint32_t* bad_count) {
@@ -461,7 +405,7 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
 #pragma unroll
         for (int r = 0; r < R; ++r) out_id[r] = r;
     }
-    const OffT o = OffT(chunk) * OffT(TB * kVecBytes) + OffT(threadIdx.x * kVecBytes);
+    const OffT o = OffT(chunk) * OffT(kThreads * kVecBytes) + OffT(threadIdx.x * kVecBytes);
     if (o >= len) return;
     const uint64_t avail = len - o;
     u32x4 acc[R];
@@ -483,14 +427,9 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
             asm volatile("" : "+s"(plan));
             tab += plan * (K * R * 5);
         }
-        if constexpr (XORONLY) {
 #pragma unroll
-            for (int i = 0; i < K; ++i) mac<R, true>(acc, d[i], tab + i * (R * 5));
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; i += 2)
-                gf_mac2<R>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
-        }
+        for (int i = 0; i < K; i += 2)
+            gf_mac2<R>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
         // Materialise every row before the uniform `r < nout` store branches:
         // otherwise the compiler sinks each row's math into its branch, keeps
         // all 200 table words live and spills SGPRs (154 VGPRs, 3 waves/SIMD).
@@ -513,37 +452,33 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
     }
 }
 
-// FAST: the shipped mapping at 256 threads with shards below 4 GiB (see
-// fast_item); otherwise the measurement mappings and 64-bit lane offsets.
-template <bool DEC, bool XORONLY, int TB, bool FAST>
-__global__ __launch_bounds__(TB) void rs104_kernel(ApplyArgs a) {
+// 16 bytes per lane, one 4 KiB column range per workgroup: the aligned
+// RS(10,4) encodes the bit-sliced kernel does not take and the decodes of
+// shard lengths that are not a multiple of 2 KiB. OffT = uint64_t for shards
+// of 4 GiB and more.
+template <bool DEC, typename OffT>
+__global__ __launch_bounds__(kThreads) void rs104_kernel(ApplyArgs a) {
     uint32_t stripe, chunk;
-    fast_item<FAST>(a, a.chunks_per_stripe, stripe, chunk);
+    fast_item(a, a.chunks_per_stripe, stripe, chunk);
     const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
-    using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
-    rs104_chunk<DEC, XORONLY, false, TB, OffT>(a.in_base + uint64_t(stripe) * a.in_stripe,
-                                               a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard,
-                                               a.out_shard, a.len, chunk, mask, as_const(a.tabs), as_const(a.lut),
-                                               a.bad_count);
+    rs104_chunk<DEC, false, OffT>(a.in_base + uint64_t(stripe) * a.in_stripe,
+                                  a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, a.len,
+                                  chunk, mask, as_const(a.tabs), as_const(a.lut), a.bad_count);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
-// RS(10,4) with 8 or 4 bytes per lane (hec_set_decode_vector_bytes /
-// hec_set_encode_vector_bytes; 2 or 1 KiB column range per workgroup,
-// dwordx2 / dword streams): less math per wave between its loads and its
-// stores, fewer VGPRs (54 for the 8 B decode), more waves per SIMD. The
-// default decode on shards that are a multiple of 2 KiB.
-// Encode (DEC=false: inputs 0..9, outputs 0..3) and the XOR-only twin
-// (XORONLY: same traffic, no GF math) are measurement forms.
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x1 __attribute__((ext_vector_type(1)));
-// One 256 * sizeof(V)-byte column range (`chunk`) of one stripe at 8 or 4
-// bytes per lane. Decode: in place (in_b == out_b), shard ids from the present
-// mask. Shards below 4 GiB (32-bit lane offsets).
-template <bool DEC, bool XORONLY, typename V>
+// RS(10,4) with 8 bytes per lane (2 KiB column range per workgroup, dwordx2
+// streams): less math per wave between its loads and its stores, 54 VGPRs
+// (8 waves/SIMD) instead of 100. The decode of shard lengths that are a
+// multiple of 2 KiB (0.9-1.7% faster than 16 B, profiles/r02/
+// ab_decode_bytes_per_lane.jsonl), and the zero-copy host encode over PCIe
+// (DEC=false: inputs 0..9, outputs 0..3; profiles/r04/e2e_encode_kernels_*).
+// Shards below 4 GiB (32-bit lane offsets).
+template <bool DEC>
 __device__ __forceinline__ void rs104_narrow_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
                                                    uint64_t out_shard, uint32_t chunk, uint32_t mask_in, cu32p tabs,
                                                    cu32p lut, uint32_t* bad_count) {
+    typedef u32x2 V;
     constexpr int K = 10, N = 14, R = 4, VB = int(sizeof(V));
     uint32_t in_id[K], out_id[R];
     uint32_t nout = R, plan = 0;
@@ -588,16 +523,9 @@ __device__ __forceinline__ void rs104_narrow_chunk(const uint8_t* in_b, uint8_t*
         V acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = V(0u);
-        if constexpr (XORONLY) {
 #pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r] ^= d[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; i += 2)
-                gf_mac2<R, V>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
-        }
+        for (int i = 0; i < K; i += 2)
+            gf_mac2<R, V>(acc, d[i], d[i + 1], tab + i * (R * 5), tab + (i + 1) * (R * 5), nout);
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -610,40 +538,38 @@ __device__ __forceinline__ void rs104_narrow_chunk(const uint8_t* in_b, uint8_t*
     }
 }
 
-template <bool DEC, bool XORONLY, typename V>
+template <bool DEC>
 __global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
     uint32_t stripe, chunk;
-    fast_item<true>(a, a.chunks_per_stripe, stripe, chunk);
+    fast_item(a, a.chunks_per_stripe, stripe, chunk);
     const uint32_t mask = DEC ? as_const(a.masks)[stripe] : 0u;
-    rs104_narrow_chunk<DEC, XORONLY, V>(a.in_base + uint64_t(stripe) * a.in_stripe,
-                                        a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, chunk,
-                                        mask, as_const(a.tabs), as_const(a.lut), a.bad_count);
+    rs104_narrow_chunk<DEC>(a.in_base + uint64_t(stripe) * a.in_stripe, a.out_base + uint64_t(stripe) * a.out_stripe,
+                            a.in_shard, a.out_shard, chunk, mask, as_const(a.tabs), as_const(a.lut), a.bad_count);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
-// Two 4 KiB chunks per workgroup (launch config vec_per_thread = 2; shard
-// length a multiple of 8 KiB): each lane issues the 20 loads of both chunks,
-// then does the math of the first while the second's loads are in flight.
-// Chunks 2p and 2p+1 share a stripe, hence shard ids and tables.
-template <bool DEC, bool XORONLY, bool FAST>
-__device__ __forceinline__ void rs104_pair_body(const ApplyArgs& a) {
-    constexpr int K = 10, N = 14, R = 4, U = 2;
-    uint32_t stripe, p;
-    fast_item<FAST>(a, a.chunks_per_stripe / U, stripe, p);
-    const uint8_t* in_b = a.in_base + uint64_t(stripe) * a.in_stripe;
-    uint8_t* out_b = a.out_base + uint64_t(stripe) * a.out_stripe;
-    uint32_t in_id[K], out_id[R];
-    uint32_t nout = R, plan = 0;
-    cu32p tab = as_const(a.tabs);
-    if constexpr (DEC) {
-        const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
-        const uint32_t present = __builtin_popcount(mask);
-        if (present < K) {
-            if (p == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
-            return;
-        }
-        if (present == N) return;
-        nout = N - present;
+// ---------------------------------------------------------------------------
+// Round-6 decode experiment (profiles/r06/INDEX.md):
+// the table decode at the bit-sliced encode's geometry -- 32 bytes per lane
+// per shard (two dwordx4 4 KiB apart), one 8 KiB column range per workgroup --
+// so each coefficient's table halves are copied into VGPRs once per 8 dwords
+// of data instead of once per 2 (the shipped 8 B decode spends 99 of its ~580
+// VALU instructions per wave on those copies). Selected only by
+// hec_set_decode_vector_bytes(32), on shard lengths that are a multiple of
+// 8 KiB below 4 GiB. All four rows are computed (padded rows multiply by 0);
+// only the erased ones are stored.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void rs104_wide_kernel(ApplyArgs a) {
+    constexpr int K = 10, N = 14, R = 4, W = 8;
+    uint32_t stripe, chunk;
+    fast_item(a, a.chunks_per_stripe, stripe, chunk);
+    uint8_t* b = a.out_base + uint64_t(stripe) * a.out_stripe;  // in place (in_base == out_base)
+    const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
+    const uint32_t present = __builtin_popcount(mask);
+    if (present < K && chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
+    if (present >= K && present < N) {
+        const uint32_t nout = N - present;
+        uint32_t in_id[K], out_id[R];
         uint32_t m = mask;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
@@ -656,109 +582,119 @@ __device__ __forceinline__ void rs104_pair_body(const ApplyArgs& a) {
             out_id[r] = e ? __builtin_ctz(e) : 0;
             e &= e - 1;
         }
-        plan = as_const(a.lut)[mask];  // first used after the data loads
-    } else {
+        uint32_t plan = as_const(a.lut)[mask];
+        const uint32_t o = chunk * (kThreads * 32) + threadIdx.x * 16;
+        uint32_t d[K][W];
 #pragma unroll
-        for (int i = 0; i < K; ++i) in_id[i] = i;
+        for (int i = 0; i < K; ++i) {
+            const u32x4 lo = load_at(b + uint64_t(in_id[i]) * a.in_shard, o);
+            const u32x4 hi = load_at(b + uint64_t(in_id[i]) * a.in_shard, o + uint32_t(kThreads * 16));
 #pragma unroll
-        for (int r = 0; r < R; ++r) out_id[r] = r;
-    }
-    using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
-    const OffT o0 = OffT(p) * OffT(U * kThreads * kVecBytes) + OffT(threadIdx.x * kVecBytes);
-    u32x4 d[U][K];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            d[u][i] = load_at(in_b + uint64_t(in_id[i]) * a.in_shard, o0 + OffT(u * (kThreads * kVecBytes)));
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (DEC) {
+            for (int w = 0; w < 4; ++w) {
+                d[i][w] = lo[w];
+                d[i][4 + w] = hi[w];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // all twenty loads in flight before the math
         asm volatile("" : "+s"(plan));
-        tab += plan * (K * R * 5);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        // Opaque per chunk: the table words are re-read (scalar cache hits)
-        // for the second chunk instead of held live across both (SGPR spills).
-        const uint64_t tb = reinterpret_cast<uint64_t>(tab);
-        uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(tb)), hi = __builtin_amdgcn_readfirstlane(uint32_t(tb >> 32));
-        asm volatile("" : "+s"(lo), "+s"(hi));
-        const cu32p t = reinterpret_cast<cu32p>((uint64_t(hi) << 32) | lo);
-        u32x4 acc[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < K; ++i) mac<R, XORONLY>(acc, d[u][i], t + i * (R * 5));
-#pragma unroll
-        for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
+        cu32p tab = as_const(a.tabs) + plan * (K * R * 5);
+        uint32_t acc[R][W];
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if (r < int(nout))
-                store_at(out_b + uint64_t(out_id[r]) * a.out_shard, o0 + OffT(u * (kThreads * kVecBytes)), acc[r]);
+#pragma unroll
+            for (int w = 0; w < W; ++w) acc[r][w] = 0;
+#pragma unroll
+        for (int i = 0; i < K; i += 2) {
+            // opaque per pair: its 40 table words are loaded here, not hoisted
+            // with the other pairs' (200 SGPRs, spilled)
+            uint64_t tp = reinterpret_cast<uint64_t>(tab + i * (R * 5));
+            uint32_t lo = uint32_t(tp), hi = uint32_t(tp >> 32);
+            asm volatile("" : "+s"(lo), "+s"(hi));
+            cu32p t0 = reinterpret_cast<cu32p>((uint64_t(hi) << 32) | lo), t1 = t0 + R * 5;
+            // the pair's 40 table words; the 16 halves a v_perm needs in a
+            // VGPR are copied once and reused by all 8 dwords of the lane
+            uint32_t ta[R * 5], tb[R * 5];
+#pragma unroll
+            for (int j = 0; j < R * 5; ++j) {
+                ta[j] = t0[j];
+                tb[j] = t1[j];
+            }
+            uint32_t va[R][2], vb[R][2];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                va[r][0] = ta[r * 5 + 1];
+                va[r][1] = ta[r * 5 + 3];
+                vb[r][0] = tb[r * 5 + 1];
+                vb[r][1] = tb[r * 5 + 3];
+                asm volatile("" : "+v"(va[r][0]), "+v"(va[r][1]), "+v"(vb[r][0]), "+v"(vb[r][1]));
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t x0 = d[i][w], x1 = d[i + 1][w];
+                const uint32_t s00 = x0 & 0x07070707u, s01 = (x0 >> 3) & 0x07070707u, s02 = (x0 >> 6) & 0x03030303u;
+                const uint32_t s10 = x1 & 0x07070707u, s11 = (x1 >> 3) & 0x07070707u, s12 = (x1 >> 6) & 0x03030303u;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t p0 = __builtin_amdgcn_perm(va[r][0], ta[r * 5 + 0], s00);
+                    const uint32_t p1 = __builtin_amdgcn_perm(va[r][1], ta[r * 5 + 2], s01);
+                    const uint32_t p2 = __builtin_amdgcn_perm(ta[r * 5 + 4], ta[r * 5 + 4], s02);
+                    const uint32_t q0 = __builtin_amdgcn_perm(vb[r][0], tb[r * 5 + 0], s10);
+                    const uint32_t q1 = __builtin_amdgcn_perm(vb[r][1], tb[r * 5 + 2], s11);
+                    const uint32_t q2 = __builtin_amdgcn_perm(tb[r * 5 + 4], tb[r * 5 + 4], s12);
+                    uint32_t x = __builtin_amdgcn_bitop3_b32(acc[r][w], p0, p1, 0x96);
+                    x = __builtin_amdgcn_bitop3_b32(x, p2, q0, 0x96);
+                    acc[r][w] = __builtin_amdgcn_bitop3_b32(x, q1, q2, 0x96);
+                }
+            }
+        }
+        // every row materialised before the uniform store branches (else the
+        // math sinks into them and the table words stay live: SGPR spills)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int w = 0; w < W; ++w) asm volatile("" ::"v"(acc[r][w]));
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r < int(nout)) {
+                uint8_t* sb = b + uint64_t(out_id[r]) * a.out_shard;
+                store_at(sb, o, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+                store_at(sb, o + uint32_t(kThreads * 16), u32x4{acc[r][4], acc[r][5], acc[r][6], acc[r][7]});
+            }
     }
-}
-
-template <bool DEC, bool XORONLY, bool FAST>
-__global__ __launch_bounds__(kThreads) void rs104_pair_kernel(ApplyArgs a) {
-    rs104_pair_body<DEC, XORONLY, FAST>(a);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
 // ---------------------------------------------------------------------------
 // Bit-sliced RS(10,4) encode (fixed parity matrix). A lane owns 32 bytes of
-// every shard (two 16-byte vectors TB*16 apart, so each load instruction stays
+// every shard (two 16-byte vectors 4 KiB apart, so each load instruction stays
 // one contiguous 1 KiB per wave). Its 8 dwords per shard are transposed into 8
 // bit planes (plane k = bit k of the 32 bytes), the 80 data planes go through
 // the generated XOR program (tools/gen_bitslice.py: 328 three-input XORs for
 // all 32 parity planes), and the parity planes are transposed back. Per data
 // dword that is ~12.5 VALU ops against ~27 for the table-lookup multiply, so
-// the math hides at lower occupancy.
+// the math hides at lower occupancy (170 VGPRs, 2 waves/SIMD).
 // ---------------------------------------------------------------------------
-// One 2*TB*16-byte column range (`chunk`) of one stripe: inputs 0..9 at in_b,
-// parity 0..3 at out_b.
-// VB = 16: two dwordx4 per lane per shard, TB*16 apart; VB = 8 (measurement,
-// hec_set_bitslice_vector_bytes): four dwordx2 per lane per shard, TB*8 apart,
-// the same 2*TB*16-byte column range. Each output byte depends only on the
-// input bytes of its own column, so the planes only need the stores to use
-// the loads' byte positions.
-template <int TB, typename OffT = uint64_t, int VB = 16>
+// One 8 KiB column range (`chunk`) of one stripe: inputs 0..9 at in_b, parity
+// 0..3 at out_b.
+template <typename OffT = uint64_t>
 __device__ __forceinline__ void rs104_bs_chunk(const uint8_t* in_b, uint8_t* out_b, uint64_t in_shard,
                                                uint64_t out_shard, uint32_t chunk) {
-    constexpr int K = 10, R = 4, NV = 32 / VB;  // vectors per lane per shard
-    static_assert(VB == 16 || VB == 8, "bit-sliced lanes load 16 or 8 bytes at a time");
-    const OffT base = OffT(chunk) * OffT(TB * 2 * kVecBytes) + OffT(threadIdx.x * VB);
+    constexpr int K = 10, R = 4;
+    const OffT base = OffT(chunk) * OffT(kBsChunk) + OffT(threadIdx.x * 16);
     uint32_t p[K * 8];
-    if constexpr (VB == 16) {
-        u32x4 d[K][2];
+    u32x4 d[K][2];
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            d[i][0] = load_at(in_b + uint64_t(i) * in_shard, base);
-            d[i][1] = load_at(in_b + uint64_t(i) * in_shard, base + OffT(TB * 16));
-        }
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                p[8 * i + w] = d[i][0][w];
-                p[8 * i + 4 + w] = d[i][1][w];
-            }
-    } else {
-        u32x2 d[K][NV];
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int v = 0; v < NV; ++v)
-                d[i][v] = __builtin_nontemporal_load(
-                    (const __attribute__((address_space(1))) u32x2*)((gcu8p)(in_b + uint64_t(i) * in_shard) + base +
-                                                                     OffT(v * TB * 8)));
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                p[8 * i + 2 * v] = d[i][v][0];
-                p[8 * i + 2 * v + 1] = d[i][v][1];
-            }
+    for (int i = 0; i < K; ++i) {
+        d[i][0] = load_at(in_b + uint64_t(i) * in_shard, base);
+        d[i][1] = load_at(in_b + uint64_t(i) * in_shard, base + OffT(kThreads * 16));
     }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            p[8 * i + w] = d[i][0][w];
+            p[8 * i + 4 + w] = d[i][1][w];
+        }
 #pragma unroll
     for (int i = 0; i < K; ++i) transpose8(p + 8 * i);
     uint32_t q[R * 8];
@@ -766,41 +702,31 @@ __device__ __forceinline__ void rs104_bs_chunk(const uint8_t* in_b, uint8_t* out
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         transpose8(q + 8 * j);
-        if constexpr (VB == 16) {
-            store_at(out_b + uint64_t(j) * out_shard, base, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]});
-            store_at(out_b + uint64_t(j) * out_shard, base + OffT(TB * 16),
-                     u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]});
-        } else {
-#pragma unroll
-            for (int v = 0; v < NV; ++v)
-                __builtin_nontemporal_store(
-                    u32x2{q[8 * j + 2 * v], q[8 * j + 2 * v + 1]},
-                    (__attribute__((address_space(1))) u32x2*)((gu8p)(out_b + uint64_t(j) * out_shard) + base +
-                                                               OffT(v * TB * 8)));
-        }
+        store_at(out_b + uint64_t(j) * out_shard, base, u32x4{q[8 * j], q[8 * j + 1], q[8 * j + 2], q[8 * j + 3]});
+        store_at(out_b + uint64_t(j) * out_shard, base + OffT(kThreads * 16),
+                 u32x4{q[8 * j + 4], q[8 * j + 5], q[8 * j + 6], q[8 * j + 7]});
     }
 }
 
-template <int TB, bool FAST, int VB = 16>
-__global__ __launch_bounds__(TB) void rs104_bs_encode_kernel(ApplyArgs a) {
+template <typename OffT>
+__global__ __launch_bounds__(kThreads) void rs104_bs_encode_kernel(ApplyArgs a) {
     uint32_t stripe, chunk;
-    fast_item<FAST>(a, a.chunks_per_stripe, stripe, chunk);
-    using OffT = typename std::conditional<FAST, uint32_t, uint64_t>::type;
-    rs104_bs_chunk<TB, OffT, VB>(a.in_base + uint64_t(stripe) * a.in_stripe,
-                                 a.out_base + uint64_t(stripe) * a.out_stripe, a.in_shard, a.out_shard, chunk);
+    fast_item(a, a.chunks_per_stripe, stripe, chunk);
+    rs104_bs_chunk<OffT>(a.in_base + uint64_t(stripe) * a.in_stripe, a.out_base + uint64_t(stripe) * a.out_stripe,
+                         a.in_shard, a.out_shard, chunk);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
-// Map entry of this workgroup: with xcd_remap, XCD x = blockIdx % 8 takes
-// the x-th eighth of the launch's entries, so the workgroups sharing an XCD
-// (and its L2) stream consecutive chunks, as in the strided kernels.
+// Map entry of this workgroup: XCD x = blockIdx % 8 takes the x-th eighth of
+// the launch's entries, so the workgroups sharing an XCD (and its L2) stream
+// consecutive chunks, as in the strided kernels. The ragged decode +2% on the
+// bench batch (with the no-op skip +10% on the mixed workload,
+// profiles/r02/ab_ragged_remap_skip.jsonl); the bit-sliced ragged encode +2%
+// at 512 mixed stripes, +7% at 4096 and +9% on uniform 4 MiB stripes
+// (profiles/r03/sweep_mixed2.jsonl).
 __device__ __forceinline__ uint32_t ragged_block(const RaggedArgs& a) {
-    uint32_t b = blockIdx.x;
-    if (a.xcd_remap) {
-        const uint32_t x = b & 7u;
-        b = x * a.map_q8 + (x < a.map_r8 ? x : a.map_r8) + (b >> 3);
-    }
-    return b + a.block_base;
+    const uint32_t b = blockIdx.x, x = b & 7u;
+    return x * a.map_q8 + (x < a.map_r8 ? x : a.map_r8) + (b >> 3) + a.block_base;
 }
 
 // Descriptor of the stripe workgroup blk works on: the kernel-argument copy
@@ -819,7 +745,7 @@ __global__ __launch_bounds__(kThreads) void rs104_bs_ragged_kernel(RaggedArgs a)
     const uint64_t off = it.off, stride = it.shard_stride;
     const uint32_t first = it.first_block;
     const uint8_t* b = a.base + off;
-    rs104_bs_chunk<kThreads, uint32_t>(b, a.base + off + 10 * stride, stride, stride, blk - first);
+    rs104_bs_chunk<uint32_t>(b, a.base + off + 10 * stride, stride, stride, blk - first);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
@@ -838,53 +764,6 @@ hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream) {
     return hipSuccess;
 }
 
-// Launch constants of fast_item: the XCD eighths of the grid and the chunks
-// per stripe as a multiply-shift divisor.
-static void set_fast_map(ApplyArgs& a, uint64_t n_blocks, uint32_t per_stripe) {
-    a.map_q8 = uint32_t(n_blocks / 8);
-    a.map_r8 = uint32_t(n_blocks % 8);
-    const FastDiv f = make_fastdiv(per_stripe);
-    a.cps_mul = f.mul;
-    a.cps_shift = f.shift;
-}
-// fast_item<true> covers the shipped mappings (XCD eighths or identity, one
-// region per XCD, with or without the per-stripe rotation) and 32-bit lane
-// offsets (shards below 4 GiB).
-static bool fast_map_ok(const LaunchConfig& cfg, uint64_t len) {
-    return (cfg.xcd_remap == 0 || cfg.xcd_remap == 1) && cfg.xcd_parts <= 1 && len <= 0xFFFFFFFFull;
-}
-
-template <int TB>
-static hipError_t launch_rs104_bs(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(TB) * 2 * kVecBytes;
-    a.chunks_per_stripe = uint32_t(a.len / chunk);
-    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
-    if (a.n_items == 0) return hipSuccess;
-    a.xcd_remap = uint32_t(cfg.xcd_remap);
-    a.xcd_parts = uint32_t(cfg.xcd_parts);
-    a.chunk_rot = uint32_t(cfg.chunk_rot);
-    set_fast_map(a, a.n_items, a.chunks_per_stripe);
-    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    if (fast_map_ok(cfg, a.len) && cfg.bs_vec_bytes == 8)
-        hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, true, 8>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream,
-                           a);
-    else if (fast_map_ok(cfg, a.len))
-        hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, true>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
-    else
-        hipLaunchKernelGGL((rs104_bs_encode_kernel<TB, false>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream, a);
-    return hipGetLastError();
-}
-
-// Bit-sliced encode: shard length a multiple of 2 * TB * 16 bytes (8 KiB at
-// the default 256 threads).
-static hipError_t launch_rs104_bs_cfg(const ApplyArgs& a, const LaunchConfig& cfg, hipStream_t stream) {
-    switch (cfg.wg_threads) {
-        case 128: return launch_rs104_bs<128>(a, cfg, stream);
-        case 512: return launch_rs104_bs<512>(a, cfg, stream);
-        default: return launch_rs104_bs<256>(a, cfg, stream);
-    }
-}
-
 // Ragged batches: every stripe has its own length, shard stride and mask
 // (degraded reads of needle intervals, mixed 64 KiB-4 MiB stripes). The host
 // lays stripes out back to back and passes a workgroup -> stripe map.
@@ -896,9 +775,8 @@ __global__ __launch_bounds__(kThreads) void rs104_ragged_kernel(RaggedArgs a) {
     const RaggedItem it = ragged_item(a, blk);
     uint8_t* b = a.base + it.off;
     uint8_t* o = COMPACT ? a.base + it.out_off : (DEC ? b : b + 10 * it.shard_stride);
-    rs104_chunk<DEC, false, COMPACT, kThreads, uint32_t>(b, o, it.shard_stride, it.shard_stride, it.len,
-                                                         blk - it.first_block, it.mask, as_const(a.tabs),
-                                                         as_const(a.lut), a.bad_count);
+    rs104_chunk<DEC, COMPACT, uint32_t>(b, o, it.shard_stride, it.shard_stride, it.len, blk - it.first_block, it.mask,
+                                        as_const(a.tabs), as_const(a.lut), a.bad_count);
     if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
 }
 
@@ -922,160 +800,33 @@ hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t str
     return hipSuccess;
 }
 
-template <bool DEC, bool XORONLY, int TB>
-static hipError_t launch_rs104_tb(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(TB) * kVecBytes;
-    a.chunks_per_stripe = uint32_t((a.len + chunk - 1) / chunk);
-    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
-    if (a.n_items == 0) return hipSuccess;
-    a.xcd_remap = uint32_t(cfg.xcd_remap);
-    a.xcd_parts = uint32_t(cfg.xcd_parts);
-    a.chunk_rot = uint32_t(cfg.chunk_rot);
-    set_fast_map(a, a.n_items, a.chunks_per_stripe);
-    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    if (TB == kThreads && fast_map_ok(cfg, a.len))
-        hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY, kThreads, true>), dim3(uint32_t(a.n_items)), dim3(TB), lds,
-                           stream, a);
-    else
-        hipLaunchKernelGGL((rs104_kernel<DEC, XORONLY, TB, false>), dim3(uint32_t(a.n_items)), dim3(TB), lds, stream,
-                           a);
-    return hipGetLastError();
-}
-
-// Workgroup size (speed only): 256 threads = one 4 KiB chunk per workgroup
-// (default); 512 / 1024 give each workgroup 8 / 16 KiB contiguous per shard.
-template <bool DEC, bool XORONLY>
-static hipError_t launch_rs104_pair(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(kThreads) * kVecBytes;
-    a.chunks_per_stripe = uint32_t(a.len / chunk);
-    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
-    if (a.n_items == 0) return hipSuccess;
-    a.xcd_remap = uint32_t(cfg.xcd_remap);
-    a.xcd_parts = uint32_t(cfg.xcd_parts);
-    a.chunk_rot = 0;  // the pair kernel has no rotated order
-    set_fast_map(a, a.n_items / 2, a.chunks_per_stripe / 2);
-    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    if (fast_map_ok(cfg, a.len))
-        hipLaunchKernelGGL((rs104_pair_kernel<DEC, XORONLY, true>), dim3(uint32_t(a.n_items / 2)), dim3(kThreads), lds,
-                           stream, a);
-    else
-        hipLaunchKernelGGL((rs104_pair_kernel<DEC, XORONLY, false>), dim3(uint32_t(a.n_items / 2)), dim3(kThreads),
-                           lds, stream, a);
-    return hipGetLastError();
-}
-
 // The kernel an aligned RS(10,4) batch with the fast plan layout runs, shared
 // by launch_apply and the name functions so a reported name is the kernel
-// that runs (speed-only knobs; every choice gives identical bytes).
-enum class Rs104Kind { Apply, Bitslice, Narrow, Pair, Wide };
-struct Rs104Pick {
-    Rs104Kind kind;
-    int vb;  // Narrow: bytes per lane per shard (8 or 4)
-};
-static bool rs104_fast_ok(uint64_t len, const LaunchConfig& cfg);
-static bool rs104_bitslice_ok(uint64_t len, const LaunchConfig& cfg);
-static Rs104Pick rs104_pick(uint64_t len, uint64_t n_stripes, bool dec, const LaunchConfig& cfg) {
+// that runs.
+enum class Rs104Kind { Apply, Bitslice, Narrow, Wide, Table };
+static Rs104Kind rs104_pick(uint64_t len, uint64_t n_stripes, bool dec, const LaunchConfig& cfg) {
+    // launch_apply sizes its stripe ranges for 4 KiB chunks; a batch whose
+    // chunks would pass one launch's workgroup limit takes the generic kernel
     const uint64_t items = (len + 4095) / 4096 * n_stripes;
-    if (!rs104_fast_ok(len, cfg) || items > kMaxLaunchBlocks) return {Rs104Kind::Apply, 16};
-    if (!dec && rs104_bitslice_ok(len, cfg))
-        return {Rs104Kind::Bitslice, cfg.bs_vec_bytes == 8 && fast_map_ok(cfg, len) ? 8 : 16};
-    const int vb = dec ? cfg.dec_vec_bytes : cfg.enc_vec_bytes;
-    const uint64_t narrow = uint64_t(kThreads) * uint64_t(vb);  // column range per workgroup
-    // (launch_apply sizes its stripe ranges for 4 KiB chunks; a narrow launch
-    // that would pass kMaxLaunchBlocks workgroups takes the 16-byte kernel)
-    if (vb < 16 && cfg.vec_per_thread == 1 && len % narrow == 0 && fast_map_ok(cfg, len) &&
-        cfg.wg_threads == kThreads && (len / narrow) * n_stripes <= kMaxLaunchBlocks)
-        return {Rs104Kind::Narrow, vb};
-    if (cfg.vec_per_thread == 2 && len % (2 * uint64_t(kThreads) * kVecBytes) == 0) return {Rs104Kind::Pair, 16};
-    return {Rs104Kind::Wide, 16};
+    if (items > kMaxLaunchBlocks) return Rs104Kind::Apply;
+    const bool off32 = len <= 0xFFFFFFFFull;
+    if (!dec && !cfg.over_pcie && len % kBsChunk == 0) return Rs104Kind::Bitslice;
+    const bool narrow = dec ? cfg.dec_vec_bytes == 8 : cfg.over_pcie;
+    if (narrow && off32 && len % kNarrowChunk == 0 && (len / kNarrowChunk) * n_stripes <= kMaxLaunchBlocks)
+        return Rs104Kind::Narrow;
+    if (dec && cfg.dec_vec_bytes == 32 && off32 && len % kBsChunk == 0) return Rs104Kind::Wide;
+    return Rs104Kind::Table;
 }
 
-template <bool DEC, bool XORONLY>
-static hipError_t launch_rs104(const ApplyArgs& a, const Rs104Pick& pick, const LaunchConfig& cfg,
-                               hipStream_t stream) {
-    if (pick.kind == Rs104Kind::Narrow) {
-        const uint64_t narrow = uint64_t(kThreads) * uint64_t(pick.vb);
-        ApplyArgs b = a;
-        b.chunks_per_stripe = uint32_t(a.len / narrow);
-        b.n_items = uint64_t(b.chunks_per_stripe) * a.n_stripes;
-        if (b.n_items == 0) return hipSuccess;
-        b.xcd_remap = uint32_t(cfg.xcd_remap);
-        b.chunk_rot = uint32_t(cfg.chunk_rot);
-        set_fast_map(b, b.n_items, b.chunks_per_stripe);
-        const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-        if (pick.vb == 8)
-            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x2>), dim3(uint32_t(b.n_items)), dim3(kThreads),
-                               lds, stream, b);
-        else
-            hipLaunchKernelGGL((rs104_narrow_kernel<DEC, XORONLY, u32x1>), dim3(uint32_t(b.n_items)), dim3(kThreads),
-                               lds, stream, b);
-        return hipGetLastError();
-    }
-    if (pick.kind == Rs104Kind::Pair) return launch_rs104_pair<DEC, XORONLY>(a, cfg, stream);
-    switch (cfg.wg_threads) {
-        case 512: return launch_rs104_tb<DEC, XORONLY, 512>(a, cfg, stream);
-        case 1024: return launch_rs104_tb<DEC, XORONLY, 1024>(a, cfg, stream);
-        default: return launch_rs104_tb<DEC, XORONLY, kThreads>(a, cfg, stream);
-    }
-}
-
-template <int K, int U, bool ALIGNED, bool XORONLY = false>
-static hipError_t launch_t(ApplyArgs a, const LaunchConfig& cfg, hipStream_t stream) {
-    const uint64_t chunk = uint64_t(U) * kThreads * kVecBytes;
-    a.chunks_per_stripe = uint32_t((a.len + chunk - 1) / chunk);
-    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
-    if (a.n_items == 0) return hipSuccess;
-    uint64_t grid = a.n_items;
-    if (cfg.max_blocks > 0 && grid > uint64_t(cfg.max_blocks)) grid = uint64_t(cfg.max_blocks);
-    if (grid > kMaxLaunchBlocks) grid = kMaxLaunchBlocks;  // grid-stride covers the rest
-    a.xcd_remap = cfg.xcd_remap ? 1u : 0u;
-    // Occupancy cap: dynamic LDS that only blocks_per_cu workgroups fit in 160 KiB.
-    const size_t lds = cfg.blocks_per_cu > 0 ? (size_t(163840) / size_t(cfg.blocks_per_cu)) & ~size_t(1023) : 0;
-    hipLaunchKernelGGL((rs_apply_kernel<K, U, ALIGNED, XORONLY>), dim3(uint32_t(grid)), dim3(kThreads), lds, stream, a);
-    return hipGetLastError();
-}
-
-// Kernel choice for an aligned RS(10,4) batch, shared by launch_apply and
-// encode_kernel_name so the name reported is the kernel that runs.
-// Fast path: one workgroup per chunk (no grid cap), 1 vector per lane, or 2
-// (pair kernel) when the shard length is a multiple of 8 KiB.
-static bool rs104_fast_ok(uint64_t len, const LaunchConfig& cfg) {
-    const bool pair_ok = cfg.vec_per_thread == 2 && len % (2 * uint64_t(kThreads) * kVecBytes) == 0;
-    return (cfg.vec_per_thread == 1 || pair_ok) && cfg.max_blocks == 0;
-}
-// Bit-sliced encode: GF mode and a shard length that is a multiple of one
-// 2 x workgroup x 16-byte column range.
-static bool rs104_bitslice_ok(uint64_t len, const LaunchConfig& cfg) {
-    return cfg.bitslice && cfg.mode == 0 && len % (uint64_t(cfg.wg_threads) * 2 * kVecBytes) == 0;
-}
-
-// Name of the kernel rs104_pick selects (one stripe: the name functions take
-// a shard length only) and its XOR-only diagnostic twin (mode 1).
-static const char* rs104_name(const Rs104Pick& p, bool dec, bool xo) {
-    switch (p.kind) {
-        case Rs104Kind::Apply:
-            return xo ? "rs_apply_kernel<10, XORONLY=true> (diagnostic)" : "rs_apply_kernel<10> (table lookup)";
-        case Rs104Kind::Bitslice:
-            return p.vb == 8 ? "rs104_bs_encode_kernel (bit-sliced, 8 B loads)" : "rs104_bs_encode_kernel (bit-sliced)";
+static const char* rs104_name(Rs104Kind k, bool dec) {
+    switch (k) {
+        case Rs104Kind::Apply: return "rs_apply_kernel<10> (table lookup)";
+        case Rs104Kind::Bitslice: return "rs104_bs_encode_kernel (bit-sliced)";
         case Rs104Kind::Narrow:
-            if (p.vb == 8)
-                return dec ? (xo ? "rs104_narrow_kernel<DEC=true, XORONLY=true, 8 B per lane> (diagnostic)"
-                                 : "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)")
-                           : (xo ? "rs104_narrow_kernel<DEC=false, XORONLY=true, 8 B per lane> (diagnostic)"
-                                 : "rs104_narrow_kernel<DEC=false, 8 B per lane> (table lookup)");
-            return dec ? (xo ? "rs104_narrow_kernel<DEC=true, XORONLY=true, 4 B per lane> (diagnostic)"
-                             : "rs104_narrow_kernel<DEC=true, 4 B per lane> (table lookup)")
-                       : (xo ? "rs104_narrow_kernel<DEC=false, XORONLY=true, 4 B per lane> (diagnostic)"
-                             : "rs104_narrow_kernel<DEC=false, 4 B per lane> (table lookup)");
-        case Rs104Kind::Pair:
-            return dec ? (xo ? "rs104_pair_kernel<DEC=true, XORONLY=true> (diagnostic)"
-                             : "rs104_pair_kernel<DEC=true> (table lookup)")
-                       : (xo ? "rs104_pair_kernel<DEC=false, XORONLY=true> (diagnostic)"
-                             : "rs104_pair_kernel<DEC=false> (table lookup)");
-        default:
-            return dec ? (xo ? "rs104_kernel<DEC=true, XORONLY=true> (diagnostic)" : "rs104_kernel<DEC=true> (table lookup)")
-                       : (xo ? "rs104_kernel<DEC=false, XORONLY=true> (diagnostic)"
-                             : "rs104_kernel<DEC=false> (table lookup)");
+            return dec ? "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)"
+                       : "rs104_narrow_kernel<DEC=false, 8 B per lane> (table lookup)";
+        case Rs104Kind::Wide: return "rs104_wide_kernel<DEC=true, 32 B per lane> (table lookup, experiment)";
+        default: return dec ? "rs104_kernel<DEC=true> (table lookup)" : "rs104_kernel<DEC=false> (table lookup)";
     }
 }
 
@@ -1083,17 +834,78 @@ constexpr const char* kNoLaunch = "none (empty shards: EmptyShard, no launch)";
 
 const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
     if (len == 0) return kNoLaunch;
-    return rs104_name(rs104_pick(len, 1, true, cfg), true, cfg.mode == 1);
+    return rs104_name(rs104_pick(len, 1, true, cfg), true);
 }
 
 const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
     if (len == 0) return kNoLaunch;
-    return rs104_name(rs104_pick(len, 1, false, cfg), false, cfg.mode == 1);
+    return rs104_name(rs104_pick(len, 1, false, cfg), false);
+}
+
+// Launch constants of fast_item: the XCD eighths of the grid and the chunks
+// per stripe as a multiply-shift divisor.
+static void set_fast_map(ApplyArgs& a, uint32_t chunk_bytes, bool round_up) {
+    a.chunks_per_stripe = uint32_t(round_up ? (a.len + chunk_bytes - 1) / chunk_bytes : a.len / chunk_bytes);
+    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
+    a.map_q8 = uint32_t(a.n_items / 8);
+    a.map_r8 = uint32_t(a.n_items % 8);
+    const FastDiv f = make_fastdiv(a.chunks_per_stripe ? a.chunks_per_stripe : 1);
+    a.cps_mul = f.mul;
+    a.cps_shift = f.shift;
+}
+
+template <bool DEC>
+static hipError_t launch_rs104(ApplyArgs a, Rs104Kind kind, hipStream_t stream) {
+    const bool off32 = a.len <= 0xFFFFFFFFull;
+    switch (kind) {
+        case Rs104Kind::Bitslice:
+            set_fast_map(a, kBsChunk, false);
+            if (a.n_items == 0) return hipSuccess;
+            if (off32)
+                hipLaunchKernelGGL((rs104_bs_encode_kernel<uint32_t>), dim3(uint32_t(a.n_items)), dim3(kThreads), 0,
+                                   stream, a);
+            else
+                hipLaunchKernelGGL((rs104_bs_encode_kernel<uint64_t>), dim3(uint32_t(a.n_items)), dim3(kThreads), 0,
+                                   stream, a);
+            break;
+        case Rs104Kind::Narrow:
+            set_fast_map(a, kNarrowChunk, false);
+            if (a.n_items == 0) return hipSuccess;
+            hipLaunchKernelGGL((rs104_narrow_kernel<DEC>), dim3(uint32_t(a.n_items)), dim3(kThreads), 0, stream, a);
+            break;
+        case Rs104Kind::Wide:
+            set_fast_map(a, kBsChunk, false);
+            if (a.n_items == 0) return hipSuccess;
+            hipLaunchKernelGGL(rs104_wide_kernel, dim3(uint32_t(a.n_items)), dim3(kThreads), 0, stream, a);
+            break;
+        default:
+            set_fast_map(a, kThreads * kVecBytes, true);
+            if (a.n_items == 0) return hipSuccess;
+            if (off32)
+                hipLaunchKernelGGL((rs104_kernel<DEC, uint32_t>), dim3(uint32_t(a.n_items)), dim3(kThreads), 0,
+                                   stream, a);
+            else
+                hipLaunchKernelGGL((rs104_kernel<DEC, uint64_t>), dim3(uint32_t(a.n_items)), dim3(kThreads), 0,
+                                   stream, a);
+            break;
+    }
+    return hipGetLastError();
+}
+
+template <int K, bool ALIGNED>
+static hipError_t launch_t(ApplyArgs a, hipStream_t stream) {
+    const uint64_t chunk = uint64_t(kThreads) * kVecBytes;
+    a.chunks_per_stripe = uint32_t((a.len + chunk - 1) / chunk);
+    a.n_items = uint64_t(a.chunks_per_stripe) * a.n_stripes;
+    if (a.n_items == 0) return hipSuccess;
+    const uint64_t grid = std::min<uint64_t>(a.n_items, kMaxLaunchBlocks);  // grid-stride covers the rest
+    hipLaunchKernelGGL((rs_apply_kernel<K, ALIGNED>), dim3(uint32_t(grid)), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
                         hipStream_t stream) {
-    // RS(10,4) fast path: fixed 4-row table stride, one chunk of >= 4 KiB per
+    // RS(10,4) fast path: fixed 4-row table stride, one chunk of >= 2 KiB per
     // workgroup and no grid-stride loop, so one launch takes at most
     // kMaxLaunchBlocks chunks: larger batches (tens of millions of short
     // stripes) go in stripe ranges.
@@ -1113,31 +925,11 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
         }
         return hipSuccess;
     }
-    const Rs104Pick pick = rs104_pick(a.len, a.n_stripes, a.masks != nullptr, cfg);
-    if (a.fast104 && aligned && pick.kind != Rs104Kind::Apply) {
-        if (a.masks) return cfg.mode == 1 ? launch_rs104<true, true>(a, pick, cfg, stream)
-                                          : launch_rs104<true, false>(a, pick, cfg, stream);
-        if (pick.kind == Rs104Kind::Bitslice) return launch_rs104_bs_cfg(a, cfg, stream);
-        return cfg.mode == 1 ? launch_rs104<false, true>(a, pick, cfg, stream)
-                             : launch_rs104<false, false>(a, pick, cfg, stream);
-    }
-    if (nin == 10 && aligned && cfg.mode == 1) {
-        switch (cfg.vec_per_thread) {
-            case 1: return launch_t<10, 1, true, true>(a, cfg, stream);
-            case 4: return launch_t<10, 4, true, true>(a, cfg, stream);
-            default: return launch_t<10, 2, true, true>(a, cfg, stream);
-        }
-    }
-    if (nin == 10 && aligned) {
-        switch (cfg.vec_per_thread) {
-            case 1: return launch_t<10, 1, true>(a, cfg, stream);
-            case 4: return launch_t<10, 4, true>(a, cfg, stream);
-            default: return launch_t<10, 2, true>(a, cfg, stream);
-        }
-    }
-    if (nin == 10) return launch_t<10, 1, false>(a, cfg, stream);
-    if (aligned) return launch_t<0, 1, true>(a, cfg, stream);
-    return launch_t<0, 1, false>(a, cfg, stream);
+    const Rs104Kind kind = rs104_pick(a.len, a.n_stripes, a.masks != nullptr, cfg);
+    if (a.fast104 && aligned && kind != Rs104Kind::Apply)
+        return a.masks ? launch_rs104<true>(a, kind, stream) : launch_rs104<false>(a, kind, stream);
+    if (nin == 10) return aligned ? launch_t<10, true>(a, stream) : launch_t<10, false>(a, stream);
+    return aligned ? launch_t<0, true>(a, stream) : launch_t<0, false>(a, stream);
 }
 
 // ---------------------------------------------------------------------------

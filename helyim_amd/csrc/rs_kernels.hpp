@@ -24,8 +24,7 @@ struct DevPlan {
 constexpr uint32_t kNoPlan = 0xFFFFFFFFu;   // mask LUT entry: too few shards present
 constexpr int kThreads = 256;               // 4 waves of 64 lanes
 // Workgroups per launch: the dispatch packet's grid is 32-bit in work-items,
-// so 2^23 workgroups (2^31 work-items at 256 threads, also at 1024 threads with
-// 4x larger chunks) keeps every launch legal.
+// so 2^23 workgroups (2^31 work-items at 256 threads) keeps every launch legal.
 constexpr uint64_t kMaxLaunchBlocks = 1ull << 23;
 constexpr int kVecBytes = 16;               // one dwordx4 per lane per access
 
@@ -47,9 +46,6 @@ struct ApplyArgs {
     const uint32_t* lut;         // mask -> plan id (used when masks != nullptr)
     uint32_t mask_limit;         // (1 << total shards) - 1: masks are clipped to the LUT
     uint32_t* bad_count;         // optional: stripes skipped for too few present shards
-    uint32_t xcd_remap;          // 1: workgroups sharing an XCD take consecutive chunks
-    uint32_t xcd_parts;          // with xcd_remap 1: regions per XCD worked on concurrently
-    uint32_t chunk_rot;          // 1: rotate each stripe's chunk order by a hash of the stripe id
     uint32_t fast104;            // 1: RS(10,4) plan set with 4-row tables; encode = plan 0 at
                                  //    offset 0, decode = tables at lut[mask] * 200 words
     // Launcher-computed workgroup -> chunk map of the RS(10,4) fast paths, so
@@ -89,7 +85,6 @@ struct RaggedArgs {
     uint32_t compact;            // decode: inputs = slots 0..9 at off (the first 10 present
                                  // shards), outputs = slots 0..e-1 at out_off (erased shards)
     uint32_t block_base;         // launcher-internal: first map entry of this launch
-    uint32_t xcd_remap;          // 1: XCD eighths of each launch's workgroups (speed only)
     uint32_t map_q8, map_r8;     // launcher-internal: that launch's workgroups / 8 and % 8
     uint32_t inline_one;         // 1: a single stripe, described by `one` (no items / map in memory)
     RaggedItem one;
@@ -102,30 +97,19 @@ hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t str
 // Bit-sliced ragged encode: every stripe's length a multiple of kBsChunk bytes;
 // the workgroup map has len / kBsChunk entries per stripe.
 constexpr uint32_t kBsChunk = 2 * kThreads * kVecBytes;  // 8 KiB
+// Column range of one workgroup of the 8-byte-per-lane table kernels.
+constexpr uint32_t kNarrowChunk = kThreads * 8;  // 2 KiB
 hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream);
 
 struct LaunchConfig {
-    int vec_per_thread = 1;      // 16-byte vectors per lane per chunk (1, 2 or 4)
-    long max_blocks = 0;         // grid cap (0 = one block per chunk)
-    int mode = 0;                // 0 = GF coding; 1 = XOR-only bandwidth ceiling (diagnostic)
-    int xcd_remap = 1;           // 0 none, 1 eighths, G>=2 runs of G chunks per XCD (speed only)
-    int blocks_per_cu = 0;       // >0: cap resident workgroups per CU via dynamic LDS (0 = no cap)
-    int xcd_parts = 1;           // with xcd_remap 1: concurrent regions per XCD (speed only)
-    int chunk_rot = 0;           // 1: hashed per-stripe rotation of chunk order (speed only)
-    int wg_threads = 256;        // RS(10,4) fast path workgroup size: 256, 512 or 1024 (speed only)
-    int dec_vec_bytes = 8;       // RS(10,4) decode bytes per lane per shard: 8 (default: dwordx2, 2 KiB
-                                 // per workgroup, on shard lengths a multiple of 2 KiB), 16 or 4 (speed only)
-    int enc_vec_bytes = 16;      // RS(10,4) table encode bytes per lane per shard: 16 (default), 8 or 4 (speed only)
-    int ragged_encode_remap = 1; // 1: XCD eighths for ragged encodes (default; 0 = dispatch order; speed only)
-    int bs_vec_bytes = 16;       // bit-sliced encode loads / stores: 16 (two dwordx4 per lane per shard,
-                                 // default) or 8 (four dwordx2; same column range; speed only)
-    int bitslice = 1;            // RS(10,4) encode on shards that are a multiple of 32 x wg_threads
-                                 // bytes: 1 = bit-sliced XOR program (default), 0 = table-lookup
-                                 // multiply (speed only)
-    int pcie_enc_narrow = 1;     // zero-copy host-batch encodes (the kernel streams host memory over
-                                 // PCIe): 1 = the 8-byte-per-lane table encode where the shard length
-                                 // is a multiple of 2 KiB (default; 3.5% faster over PCIe than the
-                                 // bit-sliced kernel), 0 = the device batches' choice (speed only)
+    int dec_vec_bytes = 8;   // RS(10,4) device decode bytes per lane per shard: 8 (default: dwordx2, 2 KiB
+                             // per workgroup, on shard lengths a multiple of 2 KiB; others take 16),
+                             // 16, or 32 (the round-6 experiment, rs104_wide_kernel; speed only)
+    bool over_pcie = false;  // set by the zero-copy host encodes (the kernel streams host memory over
+                             // PCIe): the 8-byte-per-lane table encode where the shard length is a
+                             // multiple of 2 KiB instead of the bit-sliced one (its narrower column range
+                             // per workgroup ran 50.5-52.9 against 49.4-51.1 GiB/s in 7 alternating
+                             // rounds on two boxes, profiles/r04/e2e_encode_kernels_{v,w}.jsonl)
 };
 
 // Launch one coding pass. k_fixed: number of inputs the caller guarantees

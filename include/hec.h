@@ -288,21 +288,6 @@ int hec_write_ec_files(const char* base_filename);
  * exercise the large-row path). */
 int hec_write_ec_files_ex(const char* base_filename, uint64_t buf_size, uint64_t large_block_size,
                           uint64_t small_block_size);
-/* File-level coding path (speed only; the shard bytes are the same): 0 =
- * the staged pipeline (default: pread into pinned staging, H2D, kernel, D2H,
- * pwritev); 1 = zero copy through the page cache: the .dat and the shard
- * files the GPU writes are mmap'd and registered with the GPU, the kernels
- * read and write the file pages over PCIe, the data shards of an encode are
- * written from the .dat mapping. Zero copy measured 4x slower on a 12 GiB
- * page-cached volume (registering 4 KiB pages costs more than copying them;
- * DESIGN.md §5). Where the runtime or the files refuse the mapping, a
- * zero-copy call falls back to the staged pipeline by itself. Process-wide;
- * takes effect at the next call. */
-int hec_set_file_zero_copy(int on);
-/* Process totals of file-level calls (write_ec_files / rebuild_ec_files with
- * rows to code) that ran zero copy, and of those that fell back to the staged
- * pipeline because the runtime or the files refused the mapping. */
-int hec_file_path_stats(uint64_t* zero_copy_calls, uint64_t* fallbacks);
 /* rebuild_ec_files(base_filename) -> Vec<u32> (encoder.rs:48-50, 73-109,
  * 244-307): recreates every missing .ecNN. rebuilt_ids (capacity 14) receives
  * the rebuilt shard ids in ascending order, *n_rebuilt their count. */
@@ -417,68 +402,28 @@ int hec_ec_volume_read_needles(hec_ec_volume_t* vol, const uint64_t* needle_ids,
                                uint64_t* out_offsets, int* statuses);
 
 /* ---- tuning / introspection ----------------------------------------------- */
-/* Kernel launch configuration (process-wide; speed only, results identical):
- * vec_per_thread 16-byte vectors per lane per chunk (1, 2, 4); max_blocks
- * grid cap (0 = one workgroup per 4 KiB chunk); xcd_remap: 0 none, 1 = the
- * workgroups of one XCD take a contiguous eighth of the chunks, G >= 2 = runs
- * of G consecutive chunks per XCD; blocks_per_cu > 0 caps resident
- * workgroups per CU (0 = no cap). */
-int hec_set_launch_config(int vec_per_thread, long max_blocks, int xcd_remap, int blocks_per_cu);
-/* With xcd_remap 1: the workgroups of one XCD work on `parts` regions of the
- * batch concurrently (1 = one contiguous eighth per XCD). Speed only. */
-int hec_set_xcd_parts(int parts);
-/* 1: each stripe walks its 4 KiB chunks starting at a hashed offset, so
- * concurrently running stripes touch different column ranges. Speed only. */
-int hec_set_chunk_rotation(int on);
-/* Diagnostic: 0 = GF(2^8) coding (default); 1 = XOR-only bandwidth ceiling --
- * the RS(10,4) aligned kernel with its GF math replaced by plain XOR (same
- * loads, stores and addressing; WRONG parity by design), used only to measure
- * the achievable HBM rate of this access pattern. Returns HEC_OK. */
-int hec_set_kernel_mode(int mode);
-/* Workgroup size of the RS(10,4) kernels: 256 (default; one 4 KiB chunk per
- * workgroup), 512 or 1024 (8 / 16 KiB per shard per workgroup); 128 applies to
- * the bit-sliced encode only (others use 256). Speed only. */
-int hec_set_workgroup_size(int threads);
-/* RS(10,4) device decode bytes per lane per shard: 8 (default; 2 KiB per
- * workgroup, on shard lengths that are a multiple of 2 KiB, others take 16),
- * 16 (4 KiB per workgroup) or 4 (1 KiB). Speed only. */
+/* RS(10,4) device decode bytes per lane per shard (process-wide; speed only,
+ * results identical): 8 (default; 2 KiB per workgroup, on shard lengths that
+ * are a multiple of 2 KiB, others take 16), 16 (4 KiB per workgroup), or 32
+ * (the round-6 experiment: 8 KiB per workgroup, on shard lengths that are a
+ * multiple of 8 KiB). HEC_ERR_INVALID_ARGUMENT otherwise. */
 int hec_set_decode_vector_bytes(int bytes);
-/* Same for the RS(10,4) table-lookup encode (the encodes the bit-sliced
- * kernel does not take): 16 (default), 8 or 4 bytes per lane. Speed only. */
-int hec_set_encode_vector_bytes(int bytes);
-/* RS(10,4) encode kernel on shard lengths that are a multiple of
- * 32 x workgroup size bytes (8 KiB at 256 threads): 1 = bit-sliced (bytes
- * transposed into bit planes, the fixed parity matrix applied as a generated
- * XOR program; the default), 0 = table-lookup GF multiply. Both give identical
- * parity (parity-tested); speed only. Returns HEC_OK. */
-int hec_set_encode_kernel(int kind);
-/* Bit-sliced encode memory access (measurement): 16 = two 16-byte vectors per
- * lane per shard (default), 8 = four 8-byte vectors over the same column
- * range. Identical parity; speed only. HEC_ERR_INVALID_ARGUMENT otherwise. */
-int hec_set_bitslice_vector_bytes(int bytes);
-/* Ragged device encodes (hec_gpu_encode_ragged): 1 = the workgroups of one
- * XCD take a contiguous eighth of the launch's column ranges, as the decodes
- * do with xcd_remap 1 (default; 3-9% faster on the mixed workload, DESIGN.md
- * §4), 0 = dispatch order. Applies while the global xcd_remap is 1
- * (hec_set_launch_config xcd_remap 0 turns every remap off). Speed only.
- * Returns HEC_OK. */
-int hec_set_ragged_encode_remap(int on);
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables
  * staging. Default 16 MiB (the measured crossover). Speed only. Returns HEC_OK. */
 int hec_set_host_staging(uint64_t max_bytes);
-/* Host batches on pinned memory: 1 = zero-copy kernels (default), 0 = the
- * copy pipeline. Speed only; identical results. Returns HEC_OK. */
+/* Host batches (and the per-call and degraded-read staging): 1 = zero-copy
+ * kernels that stream host memory over PCIe themselves (default), 0 = the
+ * copy pipeline: DMA copies H2D -> kernel at HBM speed -> D2H over 3 HIP
+ * streams, so the CUs are not held for the transfer (a GPU shared with other
+ * work) at a lower link rate (41-44 against 51-53 GiB/s of data, DESIGN.md
+ * section 5). Identical results. Returns HEC_OK. */
 int hec_set_host_zero_copy(int on);
-/* Zero-copy host-batch encodes (the kernel streams host memory over PCIe;
- * hec_host_encode_batch[_multi] on pinned memory and the pageable path's
- * pinned slots): 1 = the 8-byte-per-lane table encode where the shard length
- * is a multiple of 2 KiB (default: ~3.5% faster over PCIe than the bit-sliced
- * kernel), 0 = the device batches' kernel. Speed only. Returns HEC_OK. */
-int hec_set_host_encode_narrow(int on);
 /* Name of the kernel a zero-copy host-batch encode of this shard length runs
- * under the current knobs (static string). */
+ * (static string): over PCIe the 8-byte-per-lane table encode where the shard
+ * length is a multiple of 2 KiB (~3.5% faster there than the bit-sliced kernel,
+ * profiles/r04/e2e_encode_kernels_{v,w}.jsonl). */
 const char* hec_host_encode_kernel_name(uint64_t shard_len);
 /* Diagnostic: *zero_copy = 1 when [p, p + bytes) is one pinned range the
  * current device can address, i.e. host batches on it are coded zero-copy
@@ -500,15 +445,15 @@ int hec_set_completion_signal(uint64_t max_bytes);
 /* Version string of the library build. */
 const char* hec_version(void);
 /* Name of the kernel a 16-byte-aligned RS(10,4) device batch encode of this
- * shard length runs under the current launch configuration (static string;
+ * shard length runs (static string;
  * shard_len 0, which fails with HEC_ERR_EMPTY_SHARD before any launch, names
  * no kernel: "none (...)"). */
 const char* hec_encode_kernel_name(uint64_t shard_len);
 /* Same for a 16-byte-aligned in-place RS(10,4) device batch reconstruct. */
 const char* hec_decode_kernel_name(uint64_t shard_len);
-/* Kernel (and workgroup order) hec_gpu_encode_ragged (decode = 0) or
- * hec_gpu_reconstruct_ragged (decode != 0) runs on these descriptors under the
- * current knobs: the same choice the launch makes (static string). */
+/* Kernel hec_gpu_encode_ragged (decode = 0) or hec_gpu_reconstruct_ragged
+ * (decode != 0) runs on these descriptors: the same choice the launch makes
+ * (static string). */
 const char* hec_ragged_kernel_name(const hec_stripe_desc* descs, uint32_t n_stripes, int decode);
 
 #ifdef __cplusplus

@@ -18,7 +18,7 @@
 //! argument errors of libhec.
 #![allow(non_camel_case_types)]
 
-use std::os::raw::{c_char, c_int, c_long, c_void};
+use std::os::raw::{c_char, c_int, c_void};
 
 #[repr(C)]
 pub struct hec_rs_t {
@@ -186,23 +186,10 @@ extern "C" {
                                       cap: usize, out_offsets: *mut u64, statuses: *mut c_int) -> c_int;
 
     // tuning / introspection (speed only)
-    pub fn hec_set_launch_config(vec_per_thread: c_int, max_blocks: c_long, xcd_remap: c_int,
-                                 blocks_per_cu: c_int) -> c_int;
-    pub fn hec_set_xcd_parts(parts: c_int) -> c_int;
-    pub fn hec_set_chunk_rotation(on: c_int) -> c_int;
-    pub fn hec_set_kernel_mode(mode: c_int) -> c_int;
-    pub fn hec_set_workgroup_size(threads: c_int) -> c_int;
     pub fn hec_set_decode_vector_bytes(bytes: c_int) -> c_int;
-    pub fn hec_set_encode_vector_bytes(bytes: c_int) -> c_int;
-    pub fn hec_set_encode_kernel(kind: c_int) -> c_int;
-    pub fn hec_set_ragged_encode_remap(on: c_int) -> c_int;
     pub fn hec_set_host_staging(max_bytes: u64) -> c_int;
     pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;
     pub fn hec_set_host_zero_copy(on: c_int) -> c_int;
-    pub fn hec_set_file_zero_copy(on: c_int) -> c_int;
-    pub fn hec_set_bitslice_vector_bytes(bytes: c_int) -> c_int;
-    pub fn hec_file_path_stats(zero_copy_calls: *mut u64, fallbacks: *mut u64) -> c_int;
-    pub fn hec_set_host_encode_narrow(on: c_int) -> c_int;
     pub fn hec_host_encode_kernel_name(shard_len: u64) -> *const c_char;
     pub fn hec_host_zero_copy_view(p: *const c_void, bytes: u64, zero_copy: *mut c_int) -> c_int;
     pub fn hec_host_staging_stats(n_pipelines: *mut c_int, pinned_bytes: *mut u64, device_bytes: *mut u64) -> c_int;

@@ -449,22 +449,6 @@ int main(int argc, char** argv) {
     check_host_batch_multi(ors);
     check_files(argv[2]);
     check_file_errors(argv[2], 1);
-    {   /* the same file-level checks through the zero-copy path (file pages
-         * mmap'd and registered with the GPU): every call that codes rows
-         * must run zero copy, none may fall back */
-        char zdir[4096];
-        snprintf(zdir, sizeof zdir, "%s/zc", argv[2]);
-        CHECK(mkdir(zdir, 0755) == 0, "mkdir %s", zdir);
-        uint64_t zc0 = 0, fb0 = 0, zc1 = 0, fb1 = 0;
-        CHECK(hec_file_path_stats(&zc0, &fb0) == HEC_OK, "file_path_stats");
-        CHECK(hec_set_file_zero_copy(1) == HEC_OK, "set_file_zero_copy");
-        check_files(zdir);
-        check_file_errors(zdir, 1);
-        CHECK(hec_set_file_zero_copy(0) == HEC_OK, "set_file_zero_copy(0)");
-        CHECK(hec_file_path_stats(&zc1, &fb1) == HEC_OK, "file_path_stats");
-        CHECK(zc1 > zc0 && fb1 == fb0, "zero-copy calls %llu -> %llu, fallbacks %llu -> %llu",
-              (unsigned long long)zc0, (unsigned long long)zc1, (unsigned long long)fb0, (unsigned long long)fb1);
-    }
     orc_rs_free(ors);
     hec_rs_free(rs);
     printf("%s: %d failed checks\n", argv[0], g_fail);

@@ -190,51 +190,18 @@ def test_reconstruct_batch_validation_before_device():
     assert ei.value.stripe == 0
 
 
-def test_kernel_selection_knobs_host_only():
-    """Launch knobs validate their arguments and the encode-kernel report
-    follows the shard length (no device work)."""
+def test_kernel_selection_follows_the_shard_length():
+    """The encode-kernel report follows the shard length (no device work):
+    bit-sliced on multiples of 8 KiB, the 16-byte table kernel on other
+    16-byte multiples; the host-zero-copy knob takes 0 and 1."""
     import helyim_amd as H
     lib = H.lib
-    try:
-        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_bs_encode_kernel")
-        assert lib.hec_encode_kernel_name(8192).decode().startswith("rs104_bs_encode_kernel")
-        assert lib.hec_encode_kernel_name(8192 + 16).decode().startswith("rs104_kernel<DEC=false>")
-        assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_kernel<DEC=false>")
-        assert lib.hec_set_encode_kernel(0) == 0
-        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_kernel<DEC=false>")
-        assert lib.hec_set_encode_kernel(2) != 0
-        assert lib.hec_set_workgroup_size(128) == 0
-        assert lib.hec_set_encode_kernel(1) == 0
-        assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_bs_encode_kernel")  # 32 x 128 B
-        assert lib.hec_set_workgroup_size(96) != 0
-        assert lib.hec_set_kernel_mode(1) == 0
-        assert "diagnostic" in lib.hec_encode_kernel_name(1 << 20).decode()
-        assert lib.hec_set_kernel_mode(2) != 0
-        assert lib.hec_set_kernel_mode(0) == 0
-        assert lib.hec_set_bitslice_vector_bytes(8) == 0
-        assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced, 8 B loads)"
-        assert lib.hec_set_bitslice_vector_bytes(4) != 0 and lib.hec_set_bitslice_vector_bytes(16) == 0
-        assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced)"
-        assert lib.hec_set_kernel_mode(1) == 0
-        assert lib.hec_set_host_zero_copy(0) == 0 and lib.hec_set_host_zero_copy(1) == 0
-        assert lib.hec_set_kernel_mode(0) == 0 and lib.hec_set_workgroup_size(256) == 0
-        # the name follows the dispatch predicate: 4 vectors per lane or a grid
-        # cap leave the RS(10,4) fast path for the generic kernel
-        assert lib.hec_set_launch_config(4, 0, 1, 0) == 0
-        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs_apply_kernel<10>")
-        assert lib.hec_set_launch_config(1, 4096, 1, 0) == 0
-        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs_apply_kernel<10>")
-        assert lib.hec_set_launch_config(2, 0, 1, 0) == 0
-        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_bs_encode_kernel")
-        assert lib.hec_set_encode_kernel(0) == 0
-        assert lib.hec_encode_kernel_name(1 << 20).decode().startswith("rs104_pair_kernel")
-        assert lib.hec_encode_kernel_name(4096).decode().startswith("rs_apply_kernel<10>")
-    finally:
-        lib.hec_set_kernel_mode(0)
-        lib.hec_set_workgroup_size(256)
-        lib.hec_set_encode_kernel(1)
-        lib.hec_set_launch_config(1, 0, 1, 0)
-        lib.hec_set_bitslice_vector_bytes(16)
+    assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced)"
+    assert lib.hec_encode_kernel_name(8192).decode() == "rs104_bs_encode_kernel (bit-sliced)"
+    assert lib.hec_encode_kernel_name(8192 + 16).decode().startswith("rs104_kernel<DEC=false>")
+    assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_kernel<DEC=false>")
+    assert lib.hec_encode_kernel_name(17).decode().startswith("rs104_kernel<DEC=false>")
+    assert lib.hec_set_host_zero_copy(0) == 0 and lib.hec_set_host_zero_copy(1) == 0
 
 
 def test_strided_batch_geometry_checked_before_device():
@@ -267,76 +234,40 @@ def test_strided_batch_geometry_checked_before_device():
     assert lib.hec_host_encode_batch_multi(rs.handle, many, 257, P, 14 * L, L, P, 14 * L, L, L, 2) == 66
 
 
-def test_kernel_name_follows_dispatch_under_every_knob():
-    """hec_{encode,decode}_kernel_name come from the same choice the launcher
-    makes (rs104_pick): the XOR-only mode names the diagnostic twin of the
-    kernel that runs (narrow at 4/8 B per lane, pair at 2 vectors per lane),
-    and 2 vectors per lane never reports the narrow kernel (it needs 1)."""
+def test_decode_kernel_name_follows_dispatch():
+    """hec_decode_kernel_name comes from the same choice the launcher makes
+    (rs104_pick): 8 B per lane on multiples of 2 KiB (default), the 16-byte
+    table kernel otherwise or under hec_set_decode_vector_bytes(16), the
+    round-6 32 B experiment only on multiples of 8 KiB; other widths refused."""
     import helyim_amd as H
     lib = H.lib
-    L = 1 << 20
     try:
-        for mode in (0, 1):
-            for vpt in (1, 2):
-                for vb in (4, 8, 16):
-                    assert lib.hec_set_kernel_mode(mode) == 0
-                    assert lib.hec_set_launch_config(vpt, 0, 1, 0) == 0
-                    assert lib.hec_set_decode_vector_bytes(vb) == 0
-                    assert lib.hec_set_encode_vector_bytes(vb) == 0
-                    enc = lib.hec_encode_kernel_name(L).decode()
-                    dec = lib.hec_decode_kernel_name(L).decode()
-                    if vpt == 2:
-                        want_dec = "rs104_pair_kernel<DEC=true"
-                    elif vb < 16:
-                        want_dec = "rs104_narrow_kernel<DEC=true"
-                    else:
-                        want_dec = "rs104_kernel<DEC=true"
-                    assert dec.startswith(want_dec), (mode, vpt, vb, dec)
-                    assert (f"{vb} B per lane" in dec) == (vpt == 1 and vb < 16), dec
-                    if mode == 0:
-                        assert enc.startswith("rs104_bs_encode_kernel"), enc  # GF mode, 1 MiB: bit-sliced
-                    else:  # no bit-sliced XOR twin: the table kernels' twins
-                        want_enc = ("rs104_pair_kernel<DEC=false" if vpt == 2 else
-                                    "rs104_narrow_kernel<DEC=false" if vb < 16 else "rs104_kernel<DEC=false")
-                        assert enc.startswith(want_enc), (mode, vpt, vb, enc)
-                    for name in (enc, dec):
-                        assert ("XORONLY=true" in name) == (mode == 1) or name.startswith("rs104_bs"), name
-                        assert ("diagnostic" in name) == (mode == 1), name
+        assert lib.hec_decode_kernel_name(1 << 20).decode() == "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)"
+        assert lib.hec_decode_kernel_name(2048).decode().startswith("rs104_narrow_kernel<DEC=true")
+        assert lib.hec_decode_kernel_name(2048 + 16).decode().startswith("rs104_kernel<DEC=true>")
+        for bad in (0, 4, 12, 64):
+            assert lib.hec_set_decode_vector_bytes(bad) == 66
+        assert lib.hec_set_decode_vector_bytes(16) == 0
+        assert lib.hec_decode_kernel_name(1 << 20).decode().startswith("rs104_kernel<DEC=true>")
+        assert lib.hec_set_decode_vector_bytes(32) == 0
+        assert lib.hec_decode_kernel_name(1 << 20).decode().startswith("rs104_wide_kernel<DEC=true, 32 B per lane>")
+        assert lib.hec_decode_kernel_name(2048).decode().startswith("rs104_kernel<DEC=true>")
+        # the encode never takes the decode's width
+        assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced)"
     finally:
-        lib.hec_set_kernel_mode(0)
-        lib.hec_set_launch_config(1, 0, 1, 0)
         lib.hec_set_decode_vector_bytes(8)
-        lib.hec_set_encode_vector_bytes(16)
 
 
 def test_ragged_kernel_name_follows_the_launch_choice():
     """hec_ragged_kernel_name comes from the ragged launch's own pick
     (ragged_pick in intervals.cpp): bit-sliced only when every length is a
-    multiple of 8 KiB, XCD eighths unless the ragged-encode knob or the global
-    xcd_remap (the global knob now covers ragged encodes) is off."""
-    import helyim_amd as H
+    multiple of 8 KiB; every ragged launch deals each XCD an eighth."""
     import helyim_amd.batch as B
-    lib = H.lib
     aligned = [(0, 65536, 65536, 0x3FFF), (14 * 65536, 8192, 8192, 0x3FF0)]
     odd = aligned + [(14 * 65536 + 14 * 8192, 8192, 4096, 0x3FFF)]
-    try:
-        assert B.ragged_kernel_name(aligned, False) == "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
-        assert B.ragged_kernel_name(odd, False) == "rs104_ragged_kernel<DEC=false> (table lookup, XCD eighths)"
-        assert B.ragged_kernel_name(aligned, True) == "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
-        assert lib.hec_set_ragged_encode_remap(0) == 0
-        assert B.ragged_kernel_name(aligned, False).endswith("(bit-sliced, dispatch order)")
-        assert B.ragged_kernel_name(aligned, True).endswith("XCD eighths)")  # decodes follow the global knob
-        assert lib.hec_set_ragged_encode_remap(1) == 0
-        assert lib.hec_set_launch_config(1, 0, 0, 0) == 0
-        assert B.ragged_kernel_name(aligned, False).endswith("(bit-sliced, dispatch order)")
-        assert B.ragged_kernel_name(aligned, True).endswith("(table lookup, dispatch order)")
-        assert lib.hec_set_launch_config(1, 0, 1, 0) == 0
-        assert lib.hec_set_encode_kernel(0) == 0
-        assert B.ragged_kernel_name(aligned, False).startswith("rs104_ragged_kernel<DEC=false>")
-    finally:
-        lib.hec_set_ragged_encode_remap(1)
-        lib.hec_set_launch_config(1, 0, 1, 0)
-        lib.hec_set_encode_kernel(1)
+    assert B.ragged_kernel_name(aligned, False) == "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
+    assert B.ragged_kernel_name(odd, False) == "rs104_ragged_kernel<DEC=false> (table lookup, XCD eighths)"
+    assert B.ragged_kernel_name(aligned, True) == "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
 
 
 def test_host_alloc_multi_arguments_checked_before_device():
@@ -375,25 +306,15 @@ def test_every_failure_resets_the_detail_and_values(tmp_path):
 def test_host_encode_kernel_over_pcie():
     """Zero-copy host-batch encodes (the kernel streams host memory over PCIe)
     take the 8-byte-per-lane table encode where the shard length is a
-    multiple of 2 KiB (hec_set_host_encode_narrow, default on); device
-    batches keep the bit-sliced kernel; off = the device batches' choice."""
+    multiple of 2 KiB; device batches keep the bit-sliced kernel."""
     import helyim_amd as H
     lib = H.lib
     L = 1 << 20
-    try:
-        assert lib.hec_host_encode_kernel_name(L).decode().startswith("rs104_narrow_kernel<DEC=false, 8 B per lane>")
-        assert lib.hec_encode_kernel_name(L).decode().startswith("rs104_bs_encode_kernel")
-        assert lib.hec_host_encode_kernel_name(4096 + 16).decode().startswith("rs104_kernel<DEC=false>")
-        for name in (lib.hec_host_encode_kernel_name(0), lib.hec_encode_kernel_name(0), lib.hec_decode_kernel_name(0)):
-            assert name.decode().startswith("none")  # empty shards never launch
-        assert lib.hec_set_host_encode_narrow(0) == 0
-        assert lib.hec_host_encode_kernel_name(L).decode() == lib.hec_encode_kernel_name(L).decode()
-        assert lib.hec_set_host_encode_narrow(1) == 0
-        assert lib.hec_set_kernel_mode(1) == 0  # the XOR-only diagnostic is never swapped for the narrow kernel
-        assert lib.hec_host_encode_kernel_name(L).decode() == lib.hec_encode_kernel_name(L).decode()
-    finally:
-        lib.hec_set_host_encode_narrow(1)
-        lib.hec_set_kernel_mode(0)
+    assert lib.hec_host_encode_kernel_name(L).decode().startswith("rs104_narrow_kernel<DEC=false, 8 B per lane>")
+    assert lib.hec_encode_kernel_name(L).decode().startswith("rs104_bs_encode_kernel")
+    assert lib.hec_host_encode_kernel_name(4096 + 16).decode().startswith("rs104_kernel<DEC=false>")
+    for name in (lib.hec_host_encode_kernel_name(0), lib.hec_encode_kernel_name(0), lib.hec_decode_kernel_name(0)):
+        assert name.decode().startswith("none")  # empty shards never launch
 
 
 def test_batch_base_alignment_helpers():
@@ -410,21 +331,3 @@ def test_batch_base_alignment_helpers():
         B.empty_stripes(4, 14, 1 << 20, base_align=3 << 20)
     with pytest.raises(ValueError):
         B.empty_stripes(4, 14, 1 << 20, base_align=-1)
-
-
-def test_file_zero_copy_knob_and_counters():
-    """hec_set_file_zero_copy / hec_file_path_stats (the file layer's two
-    coding paths; DESIGN.md §5 "File level"): the knob takes any int, the
-    counters read without a device and do not move on calls that fail
-    before coding."""
-    import helyim_amd as H
-    lib = H.lib
-    a, b = ctypes.c_uint64(7), ctypes.c_uint64(7)
-    assert lib.hec_file_path_stats(ctypes.byref(a), ctypes.byref(b)) == 0
-    assert lib.hec_file_path_stats(None, None) == 0
-    before = (a.value, b.value)
-    for on in (1, 5, 0):
-        assert lib.hec_set_file_zero_copy(on) == 0
-    assert lib.hec_write_ec_files(b"/nonexistent/dir/vol") == 32  # HEC_ERR_IO: no .dat
-    assert lib.hec_file_path_stats(ctypes.byref(a), ctypes.byref(b)) == 0
-    assert (a.value, b.value) == before

@@ -132,6 +132,28 @@ def test_eight_rank_dry_run_assembles_the_node_line():
     usable = min(cores["affinity_cpus"], int(cores["cgroup_cpu_quota"] or cores["affinity_cpus"]))
     assert cores["cores"] == max(1, min(cores["physical_cores"], usable))
     assert cores["quota_bound"] == (cores["physical_cores"] > usable)
+    # VERDICT r05 "next" 5: the SCALE line reads directly as per-GPU
+    # efficiency: value / N, the slowest / fastest rank's own step, and every
+    # rank's encode / decode fraction (None in the GPU-free stand-in)
+    assert out["per_gpu_GiB_s"] == pytest.approx(out["value"] / 8, rel=1e-3)
+    assert out["rank_spread"] == pytest.approx(8.0, rel=1e-3)  # rank r steps (r + 1) x step_ms
+    pf = out["per_rank_frac"]
+    assert [x["rank"] for x in pf] == list(range(8))
+    assert all({"step_ms", "encode_frac", "decode_frac"} <= set(x) for x in pf)
+    assert [x["step_ms"] for x in pf] == pytest.approx([(r + 1) * step_ms for r in range(8)])
+
+
+def test_scaling_fields_of_real_rank_records():
+    """bench.scaling_fields on run_rank-shaped records: per-GPU rate, the
+    rank spread of the ranks' own HIP-event step times, each rank's fractions."""
+    sys.path.insert(0, ROOT)
+    import bench
+    recs = [{"rank": 0, "step_ms": 18.9, "encode_frac": 0.80, "decode_frac": 0.79},
+            {"rank": 1, "step_ms": 19.8, "encode_frac": 0.77, "decode_frac": 0.75}]
+    f = bench.scaling_fields(8200.0, 2, recs)
+    assert f["per_gpu_GiB_s"] == 4100.0
+    assert f["rank_spread"] == pytest.approx(19.8 / 18.9, abs=1e-4)
+    assert f["per_rank_frac"][1] == {"rank": 1, "step_ms": 19.8, "encode_frac": 0.77, "decode_frac": 0.75}
 
 
 def test_cpu_baseline_cores_sized_to_the_quota(monkeypatch):

@@ -80,13 +80,6 @@ def test_bench_mixed_leg_verified_and_named_by_the_launcher(gpu):
     assert v["erasure_counts"] == [0, 1, 2, 3, 4] and len(v["shard_lens"]) == 7
     assert m["encode"]["kernel"] == "rs104_bs_ragged_kernel (bit-sliced, XCD eighths)"
     assert m["decode"]["kernel"] == "rs104_ragged_kernel<DEC=true> (table lookup, XCD eighths)"
-    try:  # the names follow the knobs, as the launch does
-        H.lib.hec_set_ragged_encode_remap(0)
-        m2 = bench.mixed_section(rs, 1, n_stripes=96, e2e_stripes=8)
-        assert m2["encode"]["kernel"] == "rs104_bs_ragged_kernel (bit-sliced, dispatch order)"
-        assert m2["verification"]["ok"]
-    finally:
-        H.lib.hec_set_ragged_encode_remap(1)
     assert B.ragged_kernel_name([(0, 4096, 4096, 0)], False).startswith("rs104_ragged_kernel<DEC=false>")
 
 

@@ -14,34 +14,7 @@ def _sha(path):
     return O.sha256(open(path, "rb").read())
 
 
-def _path_stats():
-    import ctypes
-    import helyim_amd as H
-    a, b = ctypes.c_uint64(), ctypes.c_uint64()
-    assert H.lib.hec_file_path_stats(ctypes.byref(a), ctypes.byref(b)) == 0
-    return a.value, b.value
-
-
-@pytest.fixture(params=["zero_copy", "staged"])
-def file_path(request):
-    """Both file-level coding paths (hec_set_file_zero_copy): the staged
-    pipeline (default) and zero copy through the page cache. Under
-    zero_copy, every call that coded rows must really have run zero copy:
-    the fallback counter may not move."""
-    import helyim_amd as H
-    assert H.lib.hec_set_file_zero_copy(1 if request.param == "zero_copy" else 0) == 0
-    before = _path_stats()
-    yield request.param
-    after = _path_stats()
-    H.lib.hec_set_file_zero_copy(0)
-    if request.param == "zero_copy":
-        assert after[1] == before[1], "a file call fell back to the staged pipeline"
-        assert after[0] > before[0], "no file call ran zero copy"
-    else:
-        assert after == before
-
-
-def test_volume_30mb_encode_rebuild(gpu, golden, tmp_path, file_path):
+def test_volume_30mb_encode_rebuild(gpu, golden, tmp_path):
     import helyim_amd as H
     g = golden("volume_30mb.json")
     base = str(tmp_path / "1")
@@ -58,7 +31,7 @@ def test_volume_30mb_encode_rebuild(gpu, golden, tmp_path, file_path):
 
 
 @pytest.mark.parametrize("size", [1, 639, 640, 641, 2000, 6401, 6400 * 2 + 3, 6400 * 3])
-def test_small_geometry_vs_oracle(gpu, tmp_path, size, file_path):
+def test_small_geometry_vs_oracle(gpu, tmp_path, size):
     """Large-row path exercised with 640-byte 'large' and 32-byte 'small' blocks."""
     import helyim_amd as H
     buf, large, small = 16, 640, 32
@@ -118,7 +91,7 @@ def test_rebuild_errors(gpu, tmp_path):
     assert _sha(base + H.to_ext(3)) == shas[3]
 
 
-def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path, file_path):
+def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path):
     """Shard files smaller than 1 MiB (row = file size), mirrored by the oracle."""
     import helyim_amd as H
     rs = O.ReedSolomon(10, 4)
@@ -136,7 +109,81 @@ def test_rebuild_matches_oracle_on_odd_sizes(gpu, tmp_path, file_path):
         assert open(base + H.to_ext(i), "rb").read() == sh[i].tobytes()
 
 
-def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path, file_path):
+def _tree(base):
+    """{ext: bytes} of every .ecNN file of a volume (absent files left out)."""
+    import helyim_amd as H
+    return {i: open(base + H.to_ext(i), "rb").read() for i in range(14) if os.path.exists(base + H.to_ext(i))}
+
+
+def test_zero_byte_dat_gives_14_empty_shards(gpu, tmp_path):
+    """A 0-byte .dat (encoder.rs:62: remaining = 0): neither row loop runs
+    (:215, :228), so write_ec_files leaves the 14 files open_ec_files created
+    and truncated (:111-127) empty; the oracle's restatement agrees."""
+    import helyim_amd as H
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    for base in (a, b):
+        open(base + ".dat", "wb").close()
+        for i in (3, 12):  # stale shard files from an earlier run are truncated
+            open(base + H.to_ext(i), "wb").write(b"stale")
+    H.write_ec_files(a)
+    O.write_ec_files(b)
+    assert _tree(a) == _tree(b) == {i: b"" for i in range(14)}
+    # and a rebuild over those empty shards (the first present read is 0
+    # bytes, encoder.rs:269-271) recreates the missing one, still empty
+    os.remove(a + H.to_ext(5))
+    assert H.rebuild_ec_files(a) == [5]
+    assert _tree(a) == {i: b"" for i in range(14)}
+
+
+@pytest.mark.parametrize("short", [0, 6, 13])
+def test_rebuild_stops_when_a_present_shard_ends_a_row_early(gpu, tmp_path, short):
+    """rebuild_ec_files reads row by row in shard order and returns Ok at the
+    first present shard whose read is 0 bytes (encoder.rs:268-271), BEFORE
+    the size check (:275) and before that row is reconstructed or written:
+    with one present shard (the first, a middle or the last present one) a
+    whole 1 MiB row shorter than the others, the rebuilt shards hold only the
+    rows every present shard has. Exact sizes and bytes, product vs oracle."""
+    import helyim_amd as H
+    L = 2 << 20  # two 1 MiB rebuild rows
+    rs = O.ReedSolomon(10, 4)
+    sh = [O.splitmix64_bytes(700 + i, L) for i in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+    rs.encode(sh)
+    lost = [2, 11] if short not in (2, 11) else [3, 10]
+    trees = []
+    for name in ("a", "b"):
+        base = str(tmp_path / name)
+        for i in range(14):
+            open(base + H.to_ext(i), "wb").write(sh[i].tobytes())
+        os.truncate(base + H.to_ext(short), 1 << 20)
+        for i in lost:
+            os.remove(base + H.to_ext(i))
+        trees.append(base)
+    assert H.rebuild_ec_files(trees[0]) == lost
+    assert O.rebuild_ec_files(trees[1]) == lost
+    got, want = _tree(trees[0]), _tree(trees[1])
+    assert got == want
+    for i in lost:
+        assert len(got[i]) == 1 << 20, (i, len(got[i]))  # row 1 never written
+        assert got[i] == sh[i][: 1 << 20].tobytes()
+
+
+def test_rebuild_over_all_empty_present_shards(gpu, tmp_path):
+    """Every present shard empty: the first read returns 0 bytes at offset 0
+    (encoder.rs:269-271), so rebuild_ec_files returns the missing ids with
+    their files created (open with create + truncate: :96-103) and empty."""
+    import helyim_amd as H
+    lost = [0, 7, 10, 13]
+    bases = [str(tmp_path / n) for n in ("a", "b")]
+    for base in bases:
+        for i in range(14):
+            if i not in lost:
+                open(base + H.to_ext(i), "wb").close()
+    assert H.rebuild_ec_files(bases[0]) == lost
+    assert O.rebuild_ec_files(bases[1]) == lost
+    assert _tree(bases[0]) == _tree(bases[1]) == {i: b"" for i in range(14)}
+
+
+def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path):
     """hec_set_device per thread (hec.h): volumes encoded and rebuilt
     concurrently from several threads, round-robin over the visible devices
     (all on device 0 on a one-GPU box), each byte-identical to the fixture."""
@@ -177,7 +224,7 @@ def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path, file_pat
         assert [_sha(b + H.to_ext(i)) for i in range(14)] == g["shard_sha256"]
 
 
-def test_randomised_file_geometry_vs_oracle(gpu, tmp_path, file_path):
+def test_randomised_file_geometry_vs_oracle(gpu, tmp_path):
     """Seeded sweep of generate_ec_files over block geometries (buffer,
     large and small block sizes) and .dat sizes around the large-row rule
     (large rows only while remaining > 10 large blocks, encoder.rs:215),
@@ -217,7 +264,7 @@ def _file_digest(path):
     return h.hexdigest()
 
 
-def test_production_geometry_multi_slice_multi_job_vs_oracle(gpu, tmp_path, file_path):
+def test_production_geometry_multi_slice_multi_job_vs_oracle(gpu, tmp_path):
     """The file-layer paths a real 30,000 MB volume takes, at a size the C
     oracle finishes in seconds: 48 MiB large blocks (three 16 MiB slices per
     large block, ec_files.cpp kLargeSlice), 1 MiB small blocks, 256 KiB
@@ -274,7 +321,7 @@ def _same_file(a, b, chunk=1 << 28):
 
 
 @pytest.mark.parametrize("extra", [0, 4097])
-def test_reference_geometry_large_row_threshold(gpu, extra, file_path):
+def test_reference_geometry_large_row_threshold(gpu, extra):
     """The reference's own constants (1 GiB large blocks, 1 MiB small blocks,
     256 KiB buffers) at the large-row threshold, encoder.rs:215 (`remaining >
     large_block_size * DATA_SHARDS_COUNT`, strict): a .dat of exactly 10 GiB

@@ -355,39 +355,33 @@ def test_which_buffers_are_coded_zero_copy(gpu, host_path):
     b.close()
 
 
-@pytest.mark.parametrize("narrow", [1, 0])
 @pytest.mark.parametrize("L", [2048, 2048 * 5, 3 * 8192, 1 << 20, 4096 + 16, 4096 + 1])
-def test_host_encode_kernel_choice_over_pcie(gpu, L, narrow):
+def test_host_encode_kernel_choice_over_pcie(gpu, L):
     """Zero-copy host-batch encodes take the 8 B-per-lane table kernel for
-    shard lengths that are multiples of 2 KiB (hec_set_host_encode_narrow,
-    default on) and the device batches' choice otherwise; every choice, and a
-    batch at an odd host address (unaligned: the generic kernel), writes the
-    oracle's parity."""
+    shard lengths that are multiples of 2 KiB and the 16-byte table kernel
+    otherwise; every choice, and a batch at an odd host address (unaligned:
+    the generic kernel), writes the oracle's parity."""
     import helyim_amd as H
     import helyim_amd.batch as B
     rs = H.ReedSolomon(10, 4)
     lib = H.lib
     S = 6
-    assert lib.hec_set_host_encode_narrow(narrow) == 0
-    try:
-        name = lib.hec_host_encode_kernel_name(L).decode()
-        if narrow and L % 2048 == 0:
-            assert name.startswith("rs104_narrow_kernel<DEC=false, 8 B per lane>"), name
-        else:
-            assert name == lib.hec_encode_kernel_name(L).decode()
-        t = _host_stripes(S, L)
-        B.host_encode_batch(rs, t)
-        a = t.numpy()
-        assert np.array_equal(a[:, 10:], corc.encode_stripes(np.ascontiguousarray(a[:, :10])))
-        # the same stripes one byte into a pinned buffer: unaligned bases
-        import torch
-        raw = torch.zeros(S * 14 * L + 1, dtype=torch.uint8).pin_memory()
-        u = raw[1:].view(S, 14, L)
-        u[:, :10] = t[:, :10]
-        B.host_encode_batch(rs, u)
-        assert np.array_equal(u.numpy()[:, 10:], a[:, 10:])
-    finally:
-        lib.hec_set_host_encode_narrow(1)
+    name = lib.hec_host_encode_kernel_name(L).decode()
+    if L % 2048 == 0:
+        assert name.startswith("rs104_narrow_kernel<DEC=false, 8 B per lane>"), name
+    else:
+        assert name.startswith("rs104_kernel<DEC=false>"), name
+    t = _host_stripes(S, L)
+    B.host_encode_batch(rs, t)
+    a = t.numpy()
+    assert np.array_equal(a[:, 10:], corc.encode_stripes(np.ascontiguousarray(a[:, :10])))
+    # the same stripes one byte into a pinned buffer: unaligned bases
+    import torch
+    raw = torch.zeros(S * 14 * L + 1, dtype=torch.uint8).pin_memory()
+    u = raw[1:].view(S, 14, L)
+    u[:, :10] = t[:, :10]
+    B.host_encode_batch(rs, u)
+    assert np.array_equal(u.numpy()[:, 10:], a[:, 10:])
 
 
 @pytest.mark.parametrize("pin", [True, False])

@@ -318,31 +318,6 @@ def _stripes(S, L, seed_base=O.STRIPE_SEED_BASE):
     return t
 
 
-@pytest.mark.parametrize("S,L,pad", [(37, 3 * 8192, 0), (300, 8192, 64 << 10), (5, 1 << 20, 0), (3, 1 << 20, 16)])
-def test_bitslice_vector_bytes_identical(gpu, S, L, pad):
-    """hec_set_bitslice_vector_bytes(8) (four dwordx2 per lane per shard over
-    the same column range) writes the oracle's parity, like the default 16,
-    packed and padded (a 16-byte pad: shard bases only 16-byte aligned)."""
-    import torch
-    import helyim_amd as H
-    import helyim_amd.batch as B
-    from oracle import corc
-    t = B.empty_stripes(S, 14, L, shard_pad=pad)
-    B.fill_stripes_splitmix(t, 10, O.STRIPE_SEED_BASE)
-    try:
-        for vb in (8, 16):
-            assert H.lib.hec_set_bitslice_vector_bytes(vb) == 0
-            want = "rs104_bs_encode_kernel (bit-sliced, 8 B loads)" if vb == 8 else "rs104_bs_encode_kernel (bit-sliced)"
-            assert H.lib.hec_encode_kernel_name(L).decode() == want
-            t[:, 10:] = 0
-            B.encode_batch(H.ReedSolomon(10, 4), t)
-            torch.cuda.synchronize()
-            assert corc.check_device_batch(t) == [], vb
-    finally:
-        H.lib.hec_set_bitslice_vector_bytes(16)
-    assert H.lib.hec_set_bitslice_vector_bytes(4) != 0
-
-
 def test_fill_splitmix_matches_oracle(gpu):
     S, L = 3, 4097
     t = _stripes(S, L).cpu().numpy()
@@ -366,144 +341,69 @@ def test_batch_encode_vs_oracle(gpu, L):
     assert np.array_equal(host[:, 10:], ref)
 
 
-@pytest.mark.parametrize("ev", [8, 4])
-@pytest.mark.parametrize("L", [1024, 2048, 6144, 65536, 4096 + 16])
-def test_narrow_table_encode_vs_oracle(gpu, ev, L):
-    """hec_set_encode_vector_bytes(8 / 4) with the bit-sliced kernel off: the
-    table encode at 8 or 4 bytes per lane (rs104_narrow_kernel<DEC=false>) on
-    lengths that are a multiple of its column range, the 16-byte kernel on the
-    others; parity against the C oracle, the kernel-name report in step."""
+@pytest.mark.parametrize("dv", [8, 16, 32])
+def test_decode_widths_identical(gpu, dv):
+    """Every decode width (hec_set_decode_vector_bytes 8: the shipped 2 KiB
+    column range; 16: 4 KiB; 32: the round-6 experiment's 8 KiB) gives the
+    default's bytes on random 0-4 erasure patterns, at a length every width
+    takes and at one only the 16-byte kernel takes."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rs = H.ReedSolomon(10, 4)
-    t = _stripes(7, L)
-    H.lib.hec_set_encode_kernel(0)
-    H.lib.hec_set_encode_vector_bytes(ev)
-    try:
-        name = H.lib.hec_encode_kernel_name(L).decode()
-        assert (f"{ev} B per lane" in name) == (L % (256 * ev) == 0), name
+    for S, L in ((37, 3 * 8192), (29, 3 * 8192 + 48)):
+        t = _stripes(S, L)
         B.encode_batch(rs, t)
-        torch.cuda.synchronize()
-    finally:
-        H.lib.hec_set_encode_kernel(1)
-        H.lib.hec_set_encode_vector_bytes(16)
-    host = t.cpu().numpy()
-    assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
-
-
-@pytest.mark.parametrize("vec,max_blocks,remap,bpc,wg", [
-    (1, 0, 0, 0, 256), (1, 0, 1, 0, 256), (1, 0, 16, 0, 256), (1, 0, 256, 3, 256), (1, 97, 1, 0, 256),
-    (2, 0, 1, 0, 256), (2, 97, 0, 0, 256), (4, 0, 64, 0, 256), (4, 97, 1, 2, 256),
-    (1, 0, 1, 0, 512), (1, 0, 0, 0, 1024), (1, 0, 1, 2, 1024)])
-def test_launch_configs_identical(gpu, vec, max_blocks, remap, bpc, wg):
-    """Every launch configuration (fast and generic kernels, XCD remaps,
-    occupancy caps, workgroup sizes) produces identical encode and decode bytes."""
-    import torch
-    import helyim_amd as H
-    import helyim_amd.batch as B
-    rs = H.ReedSolomon(10, 4)
-    S, L = 37, 3 * 8192 + 48
-    t = _stripes(S, L)
-    B.set_launch_config()
-    ref = t.clone()
-    B.encode_batch(rs, ref)
-    rng = np.random.default_rng(vec * 1000 + remap)
-    masks = np.array([((1 << 14) - 1) & ~int(sum(1 << int(i) for i in rng.choice(14, int(rng.integers(0, 5)),
-                                                                                 replace=False)))
-                      for _ in range(S)], dtype=np.int32)
-    try:
-        B.set_launch_config(vec, max_blocks, remap, bpc)
-        assert H.lib.hec_set_workgroup_size(wg) == 0
-        B.encode_batch(rs, t)
-        torch.cuda.synchronize()
-        assert torch.equal(t, ref)
-        er = torch.zeros((S, 14), dtype=torch.bool)
-        for s in range(S):
-            for i in range(14):
-                er[s, i] = not (masks[s] >> i) & 1
-        er = er.cuda()
-        t[er] = 0
-        B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
-        torch.cuda.synchronize()
-        assert torch.equal(t, ref)
-    finally:
-        B.set_launch_config()
-        H.lib.hec_set_workgroup_size(256)
-
-
-@pytest.mark.parametrize("remap,bpc", [(1, 0), (0, 2), (1, 3)])
-def test_pair_kernel_identical(gpu, remap, bpc):
-    """Two chunks per workgroup (vec_per_thread 2, shard length a multiple of
-    8 KiB) gives the default kernel's bytes for encode and every-mask decode."""
-    import torch
-    import helyim_amd as H
-    import helyim_amd.batch as B
-    rs = H.ReedSolomon(10, 4)
-    S, L = 301, 5 * 8192
-    t = _stripes(S, L)
-    ref = t.clone()
-    B.encode_batch(rs, ref)
-    rng = np.random.default_rng(remap * 10 + bpc)
-    pats = [c for e in range(0, 6) for c in itertools.combinations(range(14), e)]
-    masks = np.array([((1 << 14) - 1) & ~sum(1 << i for i in pats[int(j)])
-                      for j in rng.integers(0, len(pats), S)], dtype=np.int32)
-    try:
-        B.set_launch_config(2, 0, remap, bpc)
-        B.encode_batch(rs, t)
-        torch.cuda.synchronize()
-        assert torch.equal(t, ref)
+        ref = t.clone()
+        rng = np.random.default_rng(dv * 1000 + L)
+        masks = np.array([((1 << 14) - 1) & ~int(sum(1 << int(i) for i in rng.choice(14, int(rng.integers(0, 5)),
+                                                                                     replace=False)))
+                          for _ in range(S)], dtype=np.int32)
         er = torch.from_numpy(((masks[:, None] >> np.arange(14)[None, :]) & 1) == 0).cuda()
-        t[er] = 0
-        B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
-        torch.cuda.synchronize()
-        ok = torch.from_numpy(np.array([bin(int(m)).count("1") >= 10 for m in masks])).cuda()
-        assert torch.equal(t[ok], ref[ok])
-    finally:
-        B.set_launch_config()
+        t[er] = 0x5A
+        try:
+            assert H.lib.hec_set_decode_vector_bytes(dv) == 0
+            name = H.lib.hec_decode_kernel_name(L).decode()
+            assert ("32 B per lane" in name) == (dv == 32 and L % 8192 == 0), name
+            assert ("8 B per lane" in name) == (dv == 8 and L % 2048 == 0), name
+            B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
+            torch.cuda.synchronize()
+        finally:
+            H.lib.hec_set_decode_vector_bytes(8)
+        assert torch.equal(t, ref), (dv, L)
 
 
-@pytest.mark.parametrize("kind,wg,remap,bpc", [(0, 256, 1, 0), (1, 256, 1, 0), (1, 256, 0, 2), (1, 128, 1, 3),
-                                               (1, 128, 0, 0), (1, 512, 1, 0)])
-def test_bitslice_encode_matches_oracle(gpu, kind, wg, remap, bpc):
-    """The encode kernels (hec_set_encode_kernel 0: table lookup; 1: bit-sliced,
-    at 128 / 256 / 512 threads) against
-    the C oracle: lengths that are a multiple of 32 x workgroup size take them,
-    others fall back to the table kernel; in-place [S][14][L] and separate
-    data/parity buffers."""
+def test_bitslice_encode_matches_oracle(gpu):
+    """The encode kernels against the C oracle: lengths that are a multiple of
+    8 KiB take the bit-sliced kernel, other 16-byte multiples the table
+    kernel; in-place [S][14][L] and separate data/parity buffers."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rs = H.ReedSolomon(10, 4)
-    try:
-        assert H.lib.hec_set_encode_kernel(kind) == 0
-        assert H.lib.hec_set_workgroup_size(wg) == 0
-        B.set_launch_config(1, 0, remap, bpc)
-        for S, L in ((5, 8192), (3, 3 * 8192), (2, 1 << 20), (4, 8192 + 16), (3, 4096), (700, 16384)):
-            t = _stripes(S, L)
-            B.encode_batch(rs, t)
-            torch.cuda.synchronize()
-            host = t.cpu().numpy()
-            ref = corc.encode_stripes(np.ascontiguousarray(host[:, :10]))
-            assert np.array_equal(host[:, 10:], ref), (S, L)
-            data = t[:, :10].contiguous()
-            par = torch.zeros((S, 4, L), dtype=torch.uint8, device="cuda")
-            B.encode_batch_sep(rs, data, par)
-            torch.cuda.synchronize()
-            assert np.array_equal(par.cpu().numpy(), ref), (S, L)
-        # every byte value in every shard position (all 256 x 10 inputs)
-        S, L = 10, 8192
-        t = torch.zeros((S, 14, L), dtype=torch.uint8, device="cuda")
-        for s in range(S):
-            t[s, s] = torch.arange(L, device="cuda").to(torch.uint8)
+    for S, L in ((5, 8192), (3, 3 * 8192), (2, 1 << 20), (4, 8192 + 16), (3, 4096), (700, 16384)):
+        assert H.lib.hec_encode_kernel_name(L).decode().startswith(
+            "rs104_bs_encode_kernel" if L % 8192 == 0 else "rs104_kernel<DEC=false>")
+        t = _stripes(S, L)
         B.encode_batch(rs, t)
         torch.cuda.synchronize()
         host = t.cpu().numpy()
-        assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
-    finally:
-        H.lib.hec_set_encode_kernel(1)
-        H.lib.hec_set_workgroup_size(256)
-        B.set_launch_config()
+        ref = corc.encode_stripes(np.ascontiguousarray(host[:, :10]))
+        assert np.array_equal(host[:, 10:], ref), (S, L)
+        data = t[:, :10].contiguous()
+        par = torch.zeros((S, 4, L), dtype=torch.uint8, device="cuda")
+        B.encode_batch_sep(rs, data, par)
+        torch.cuda.synchronize()
+        assert np.array_equal(par.cpu().numpy(), ref), (S, L)
+    # every byte value in every shard position (all 256 x 10 inputs)
+    S, L = 10, 8192
+    t = torch.zeros((S, 14, L), dtype=torch.uint8, device="cuda")
+    for s in range(S):
+        t[s, s] = torch.arange(L, device="cuda").to(torch.uint8)
+    B.encode_batch(rs, t)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    assert np.array_equal(host[:, 10:], corc.encode_stripes(np.ascontiguousarray(host[:, :10])))
 
 
 def test_batch_encode_separate_and_unaligned(gpu):
@@ -545,15 +445,15 @@ def test_batch_reconstruct_every_pattern(gpu):
     assert torch.equal(t, good)
 
 
-@pytest.mark.parametrize("vec", ["16B", 2, "8B", "4B"])
+@pytest.mark.parametrize("vec", [16, 8, 32])
 @pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192 + 16, 2048 * 5])
 def test_decode_kernels_every_pattern(gpu, vec, L):
     """The RS(10,4) decode kernels (16 bytes per lane over one 4 KiB chunk per
-    workgroup, the pair kernel's two chunks, or 8 / 4 bytes per lane over
-    2 / 1 KiB) with all ten loads issued before the math: all 1470
-    patterns (erased slots poisoned), plus an all-present stripe (no-op) and
-    two with too few present (skipped, counted), vs the originals; the
-    kernel-name report follows the launch configuration."""
+    workgroup, 8 bytes per lane over 2 KiB -- the default --, and the round-6
+    32-byte experiment over 8 KiB) with all loads issued before the math: all
+    1470 patterns (erased slots poisoned), plus an all-present stripe (no-op)
+    and two with too few present (skipped, counted), vs the originals; the
+    kernel-name report follows the width and the length."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -571,17 +471,14 @@ def test_decode_kernels_every_pattern(gpu, vec, L):
     masks[-2] = (1 << 14) - 1 - 0b11111           # 9 present
     masks[-1] = (1 << 14) - 1 - (0b1111 << 10) - 1  # 9 present, all parity gone
     try:
-        B.set_launch_config(vec_per_thread=2 if vec == 2 else 1)
-        H.lib.hec_set_decode_vector_bytes({"8B": 8, "4B": 4}.get(vec, 16))
+        assert H.lib.hec_set_decode_vector_bytes(vec) == 0
         name = H.lib.hec_decode_kernel_name(L).decode()
-        assert ("pair" in name) == (vec == 2 and L % 8192 == 0), name
-        assert ("8 B per lane" in name) == (vec == "8B" and L % 2048 == 0), name
-        assert ("4 B per lane" in name) == (vec == "4B" and L % 1024 == 0), name
+        assert ("8 B per lane" in name) == (vec == 8 and L % 2048 == 0), name
+        assert ("32 B per lane" in name) == (vec == 32 and L % 8192 == 0), name
         bad = torch.zeros(1, dtype=torch.int32, device="cuda")
         B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda(), bad)
         torch.cuda.synchronize()
     finally:
-        B.set_launch_config()
         H.lib.hec_set_decode_vector_bytes(8)
     assert int(bad.item()) == 2
     assert torch.equal(t, good)
@@ -1013,8 +910,8 @@ def test_randomised_device_batches_vs_oracle(gpu):
     """Seeded sweep over the device batch API: shard lengths (tiny, odd,
     16-byte and 8 KiB multiples), shard pitches (tight, padded, unaligned),
     in-place and separate parity buffers, per-stripe erasure patterns, and
-    every kernel-selection knob (encode kernel, workgroup size, XCD remap,
-    vectors per lane), all against the C oracle."""
+    every decode width (8, 16 and the 32-byte experiment), all against the C
+    oracle."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -1028,9 +925,7 @@ def test_randomised_device_batches_vs_oracle(gpu):
             S = int(rng.integers(1, 9))
             pad = int(rng.choice([0, 16, 48, 4096, 3]))
             sep = bool(rng.integers(0, 2))
-            assert lib.hec_set_encode_kernel(int(rng.integers(0, 2))) == 0
-            assert lib.hec_set_workgroup_size(int(rng.choice([128, 256, 512]))) == 0
-            B.set_launch_config(vec_per_thread=int(rng.choice([1, 2])), xcd_remap=int(rng.integers(0, 2)))
+            assert lib.hec_set_decode_vector_bytes(int(rng.choice([8, 16, 32]))) == 0
             P = L + pad
             raw = torch.zeros(S * 14 * P + 16, dtype=torch.uint8, device="cuda")
             t = raw[:S * 14 * P].view(S, 14, P)[:, :, :L]
@@ -1060,30 +955,23 @@ def test_randomised_device_batches_vs_oracle(gpu):
             assert int(bad.item()) == 0
             assert np.array_equal(t.cpu().numpy(), host), (case, L, S, pad, "decode")
     finally:
-        lib.hec_set_encode_kernel(1)
-        lib.hec_set_workgroup_size(256)
-        B.set_launch_config()
+        lib.hec_set_decode_vector_bytes(8)
 
 
 def test_randomised_ragged_batches_vs_oracle(gpu):
     """Seeded sweep over ragged device batches: per-stripe lengths (all 8 KiB
     multiples -> bit-sliced ragged encode, or mixed -> table kernel), padded
-    strides and gaps, 0..5 erasures per stripe (5 = skipped and counted); the
-    ragged encode's XCD remap on (default) and off (every third case)."""
+    strides and gaps, 0..5 erasures per stripe (5 = skipped and counted)."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rng = np.random.default_rng(1016)
     rs = H.ReedSolomon(10, 4)
-    try:
-        _ragged_sweep(H, B, torch, rng, rs)
-    finally:
-        H.lib.hec_set_ragged_encode_remap(1)
+    _ragged_sweep(H, B, torch, rng, rs)
 
 
 def _ragged_sweep(H, B, torch, rng, rs):
     for case in range(40):
-        assert H.lib.hec_set_ragged_encode_remap(0 if case % 3 == 0 else 1) == 0
         n = int(rng.integers(1, 25))
         if case % 2:
             lens = [8192 * int(rng.integers(1, 9)) for _ in range(n)]
@@ -1162,45 +1050,6 @@ def test_padded_batch_layout(gpu, L, pad):
     assert np.array_equal(t.cpu().numpy(), full)
     gaps = raw.view(S * 14, L + pad)[:, L:]
     assert bool((gaps == 0xA5).all())
-
-
-@pytest.mark.parametrize("enc_kernel,dec_vec", [(1, 8), (0, 16), (1, 4), (0, 8)])
-def test_chunk_rotation_identical(gpu, enc_kernel, dec_vec):
-    """hec_set_chunk_rotation(1) (each stripe's chunk order rotated by a hash
-    of the stripe id, on the fast SALU mapping) gives the unrotated bytes for
-    the bit-sliced and table encodes and the 4 / 8 / 16-byte decodes, on
-    lengths where the narrow kernels run and where they do not."""
-    import torch
-    import helyim_amd as H
-    import helyim_amd.batch as B
-    rs = H.ReedSolomon(10, 4)
-    rng = np.random.default_rng(enc_kernel * 100 + dec_vec)
-    try:
-        for S, L in ((37, 3 * 8192), (300, 8192), (5, 1 << 20), (9, 4096 + 48)):
-            t = _stripes(S, L)
-            B.set_launch_config()
-            ref = t.clone()
-            B.encode_batch(rs, ref)
-            masks = np.array([0x3FFF & ~int(sum(1 << int(i) for i in rng.choice(14, int(rng.integers(0, 5)),
-                                                                                replace=False)))
-                              for _ in range(S)], dtype=np.int32)
-            assert H.lib.hec_set_encode_kernel(enc_kernel) == 0
-            assert H.lib.hec_set_decode_vector_bytes(dec_vec) == 0
-            assert H.lib.hec_set_chunk_rotation(1) == 0
-            B.encode_batch(rs, t)
-            torch.cuda.synchronize()
-            assert torch.equal(t, ref), (S, L)
-            er = torch.from_numpy(((masks[:, None] >> np.arange(14)[None, :]) & 1) == 0).cuda()
-            t[er] = 0
-            B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
-            torch.cuda.synchronize()
-            assert torch.equal(t, ref), (S, L, "decode")
-            H.lib.hec_set_chunk_rotation(0)
-    finally:
-        H.lib.hec_set_chunk_rotation(0)
-        H.lib.hec_set_encode_kernel(1)
-        H.lib.hec_set_decode_vector_bytes(8)
-        B.set_launch_config()
 
 
 def test_ragged_and_batched_reconstruct_every_pattern(gpu):

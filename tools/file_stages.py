@@ -5,9 +5,9 @@ seconds (user + system, all threads) beside its wall time, and the cgroup's
 CPU quota: CPU-seconds near quota x wall means the call is CPU-bound.
 Measurement only.
 
-python tools/file_stages.py [--gib 12] [--reps 2] [--paths zero_copy,staged]
-Each path (hec_set_file_zero_copy) gets its own encode and rebuild series,
-the paths alternating call by call so both see the same page-cache state.
+python tools/file_stages.py [--gib 12] [--reps 2]
+(The round-5 zero-copy file path this tool also timed was removed in round 6:
+profiles/r05/file_stages_b.json.)
 """
 import argparse
 import json
@@ -43,9 +43,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--fresh", action="store_true", help="delete the shard files before each timed encode")
     ap.add_argument("--dir", default="/dev/shm", help="filesystem to run on (default tmpfs: page-cache rate)")
-    ap.add_argument("--paths", default="zero_copy,staged")
     args = ap.parse_args()
-    paths = args.paths.split(",")
+    paths = ["staged"]
     import helyim_amd as H
     from tools.bench_files import make_volume
     d = tempfile.mkdtemp(prefix="hec_stages_", dir=args.dir)
@@ -59,7 +58,6 @@ def main():
         H.write_ec_files(base)  # warm-up: device tables, pinned staging
         for _ in range(args.reps):
             for p in paths:
-                H.lib.hec_set_file_zero_copy(1 if p == "zero_copy" else 0)
                 r = out["paths"][p]
                 if args.fresh:
                     for i in range(14):
@@ -70,7 +68,6 @@ def main():
                 r["encode_cpu_s"].append(round(cpu_s() - c0, 3))
         for _ in range(args.reps):
             for p in paths:
-                H.lib.hec_set_file_zero_copy(1 if p == "zero_copy" else 0)
                 r = out["paths"][p]
                 for i in (0, 5, 10, 13):
                     os.remove(base + H.to_ext(i))
@@ -78,15 +75,10 @@ def main():
                 H.rebuild_ec_files(base)
                 r["rebuild_s"].append(round(time.perf_counter() - t0, 4))
                 r["rebuild_cpu_s"].append(round(cpu_s() - c0, 3))
-        H.lib.hec_set_file_zero_copy(0)  # the default
         for p in paths:
             r = out["paths"][p]
             r["encode_GiB_s"] = round(args.gib / min(r["encode_s"]), 3)
             r["rebuild_GiB_s"] = round(args.gib / min(r["rebuild_s"]), 3)
-        import ctypes
-        a, b = ctypes.c_uint64(), ctypes.c_uint64()
-        H.lib.hec_file_path_stats(ctypes.byref(a), ctypes.byref(b))
-        out["zero_copy_calls"], out["zero_copy_fallbacks"] = a.value, b.value
         print(json.dumps(out), flush=True)
     finally:
         shutil.rmtree(d, ignore_errors=True)

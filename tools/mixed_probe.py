@@ -38,7 +38,6 @@ def main():
                     help=">= 0: every stripe exactly this many erasures, lengths still mixed (separates the e mix)")
     ap.add_argument("--pads", default="0", help="gap after every shard, one layout per value")
     ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes), per round")
-    ap.add_argument("--enc-remaps", default="1", help="ragged encode XCD remap (hec_set_ragged_encode_remap), per round")
     ap.add_argument("--orders", default="given",
                     help="descriptor order of the ragged calls, per round: given (stripe order) or dealt "
                          "(each erasure count's stripes split into 8 parts of equal workgroup counts, part x of "
@@ -127,10 +126,9 @@ def main():
     kinds = ["ragged"] + (["strided"] if args.strided and (args.uniform or args.fixed_len) else [])
     mask_t = torch.tensor(masks, dtype=torch.int32, device="cuda")
     for r, p, dv, er, kind, order in ((r, p, int(dv), int(er), k, o) for r in range(args.rounds) for p in pads
-                                      for dv in args.decvecs.split(",") for er in args.enc_remaps.split(",")
+                                      for dv in args.decvecs.split(",") for er in ("1",)
                                       for k in kinds for o in (orders if k == "ragged" else ["given"])):
         H.lib.hec_set_decode_vector_bytes(dv)
-        H.lib.hec_set_ragged_encode_remap(er)
         descs = lays[p][0]
         L0 = int(Ls[0])
         view = dev.as_strided((n, 14, L0), (14 * (L0 + p), L0 + p, 1))
@@ -165,7 +163,6 @@ def main():
                           "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3),
                           "enc_bytes": int(enc_b), "dec_bytes": int(dec_b)}), flush=True)
     H.lib.hec_set_decode_vector_bytes(8)
-    H.lib.hec_set_ragged_encode_remap(1)
     descs = lays[pads[0]][0]
     if args.grouped:
         del dev

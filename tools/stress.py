@@ -9,8 +9,7 @@ Worker threads run, for --seconds, a random mix of:
   * file-level write_ec_files / rebuild_ec_files on small volumes,
   * device batches on a private torch stream,
   * device-resident ragged encode + reconstruct on a private stream,
-  * the staging census (hec_host_staging_stats) and the file layer's coding
-    path (hec_set_file_zero_copy) flipped under the other threads,
+  * the staging census (hec_host_staging_stats) under the other threads,
 every result checked bit-exact against the C oracle. Prints one JSON line.
 Measurement / test tool only.
 
@@ -171,14 +170,11 @@ def main():
 
     def knobs(rng):
         # the staging census while other threads' host batches are in flight
-        # (it must not stall their leases), and the file layer's coding path
-        # flipped under the other threads' file calls (both paths give the
-        # same bytes, so every file check holds either way)
+        # (it must not stall their leases)
         import ctypes
         n, pin, dev = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
         assert H.lib.hec_host_staging_stats(ctypes.byref(n), ctypes.byref(pin), ctypes.byref(dev)) == 0
         assert 0 <= n.value <= 8, n.value
-        assert H.lib.hec_set_file_zero_copy(int(rng.integers(0, 2))) == 0
         note("knobs")
 
     def worker(t_id):

@@ -42,10 +42,11 @@ def trace_key(bench_kernel_name):
 
 
 def matches(trace_name, key):
+    """A template kernel demangles as base<args>(...), a plain one as base(...)."""
     base, dec = key
     i = trace_name.find(base + "<")
     if i < 0:
-        return False
+        return dec is None and (base + "(") in trace_name
     return dec is None or trace_name[i + len(base) + 1:].startswith(dec)
 
 

@@ -89,7 +89,6 @@ SIGNATURES = {
     "hec_ec_volume_read_needles": (_I, [_P, _P, _S, _P, _S, _P, _P]),
     "hec_set_host_staging": (_I, [ctypes.c_uint64]),
     "hec_set_completion_signal": (_I, [ctypes.c_uint64]),
-    "hec_set_decode_vector_bytes": (_I, [_I]),
     "hec_set_host_zero_copy": (_I, [_I]),
     "hec_host_encode_kernel_name": (ctypes.c_char_p, [ctypes.c_uint64]),
     "hec_host_zero_copy_view": (_I, [_P, _U64, ctypes.POINTER(_I)]),

@@ -180,24 +180,6 @@ void pool_run(size_t n, unsigned max_threads, const std::function<void(size_t)>&
     for (size_t i = 0; i < n; ++i) fn(i);  // every pool of this device busy: this thread alone
 }
 
-// Process-wide launch knobs (hec_set_decode_vector_bytes; speed only): set under a
-// mutex, read as a snapshot per launch, so concurrent callers never see a
-// half-updated configuration.
-namespace {
-std::mutex g_cfg_mu;
-LaunchConfig g_cfg;
-}  // namespace
-
-LaunchConfig launch_config() {
-    std::lock_guard<std::mutex> lk(g_cfg_mu);
-    return g_cfg;
-}
-
-static void update_launch_config(const std::function<void(LaunchConfig&)>& f) {
-    std::lock_guard<std::mutex> lk(g_cfg_mu);
-    f(g_cfg);
-}
-
 int current_device(int* dev) {
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
@@ -419,21 +401,10 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
     const uint64_t align = uint64_t(reinterpret_cast<uintptr_t>(in_base)) | in_stripe | in_shard |
                            uint64_t(reinterpret_cast<uintptr_t>(out_base)) | out_stripe | out_shard;
     const bool aligned = (align % 16) == 0;
-    const LaunchConfig cfg = over_pcie && !masks ? pcie_encode_config(launch_config()) : launch_config();
-    HEC_HIP(launch_apply(a, int(nin), aligned, cfg, s));
+    HEC_HIP(launch_apply(a, int(nin), aligned, over_pcie && !masks, s));
     return HEC_OK;
 }
 
-// Over PCIe the encode's bytes arrive at the link's rate, so its VALU cost is
-// free and the narrower column range per workgroup wins: the 8 B-per-lane
-// table encode ran 50.5-52.9 GiB/s of data against 49.4-51.1 for the
-// bit-sliced kernel on 512 x 1 MiB pinned stripes, alternating in one process
-// on two boxes, ahead in each of the 7 rounds (profiles/r04/e2e_encode_kernels_*.jsonl, profiles/r04/INDEX.md).
-LaunchConfig pcie_encode_config(const LaunchConfig& cfg) {
-    LaunchConfig c = cfg;
-    c.over_pcie = true;
-    return c;
-}
 
 // ---------------------------------------------------------------------------
 // Per-device scratch for host-memory calls
@@ -757,18 +728,12 @@ int hec_get_device(int* device) {
     return current_device(device);
 }
 
-const char* hec_encode_kernel_name(uint64_t shard_len) { return encode_kernel_name(shard_len, launch_config()); }
-const char* hec_decode_kernel_name(uint64_t shard_len) { return decode_kernel_name(shard_len, launch_config()); }
+const char* hec_encode_kernel_name(uint64_t shard_len) { return encode_kernel_name(shard_len, false); }
+const char* hec_decode_kernel_name(uint64_t shard_len) { return decode_kernel_name(shard_len); }
 
-int hec_set_decode_vector_bytes(int bytes) {
-    if (bytes != 8 && bytes != 16 && bytes != 32)
-        return fail(HEC_ERR_INVALID_ARGUMENT, "decode vector bytes must be 8, 16 or 32");
-    update_launch_config([&](LaunchConfig& c) { c.dec_vec_bytes = bytes; });
-    return HEC_OK;
-}
 
 const char* hec_host_encode_kernel_name(uint64_t shard_len) {
-    return encode_kernel_name(shard_len, pcie_encode_config(launch_config()));
+    return encode_kernel_name(shard_len, true);
 }
 
 int hec_set_host_staging(uint64_t max_bytes) {

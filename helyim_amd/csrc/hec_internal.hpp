@@ -130,7 +130,6 @@ struct GeomDevice {
 int geom_device(const hec_rs* rs, GeomDevice** out);
 int ensure_dense_decode(const hec_rs* rs, GeomDevice* gd, hipStream_t s);
 
-LaunchConfig launch_config();  // snapshot of the process-wide knobs
 int current_device(int* dev);
 
 // Completion of one small host call without hipStreamSynchronize: the
@@ -307,8 +306,5 @@ int run_apply(const DevicePlanSet& ps, uint32_t nin, const uint8_t* in_base, uin
               uint64_t in_shard, uint8_t* out_base, uint64_t out_stripe, uint64_t out_shard,
               uint64_t len, uint32_t n_stripes, const uint32_t* masks, uint32_t* bad,
               hipStream_t s, Completion* done = nullptr, bool over_pcie = false);
-// The launch configuration a zero-copy host-batch encode (kernel streaming
-// host memory over PCIe) runs under: the knobs, with pcie_enc_narrow applied.
-LaunchConfig pcie_encode_config(const LaunchConfig& cfg);
 
 }  // namespace hec

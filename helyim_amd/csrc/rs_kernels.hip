@@ -22,13 +22,13 @@
 //    (rs104_bs_encode_kernel): the fixed parity matrix as a generated XOR
 //    program over bit planes, half the table multiply's VALU work.
 //
-// Every kernel here is a product path (rs104_pick / ragged_pick choose among
-// them by shard length and alignment), except rs104_wide_kernel, the round-6
-// decode experiment selected only by hec_set_decode_vector_bytes(32).
-// Variants measured and not kept (XOR-only twins, the pair kernel, chunk
-// rotation, 128/512/1024-thread launches, 4 B and 8 B-load variants,
-// occupancy caps) are in git history and profiles/r0*/INDEX.md; the math-free
-// stream ceilings live in tools/membench.hip.
+// Every kernel here is a product path: rs104_pick / ragged_pick choose among
+// them by shard length, alignment and where the bytes live. Variants measured
+// and not kept (XOR-only twins, the pair kernel, chunk rotation,
+// 128/512/1024-thread launches, 4 B and 8 B-load variants, occupancy caps, the
+// round-6 32-byte-per-lane table decode) are in git history and
+// profiles/r0*/INDEX.md; the math-free stream ceilings live in
+// tools/membench.hip.
 #include <algorithm>
 #include <type_traits>
 
@@ -549,122 +549,6 @@ __global__ __launch_bounds__(kThreads) void rs104_narrow_kernel(ApplyArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Round-6 decode experiment (profiles/r06/INDEX.md):
-// the table decode at the bit-sliced encode's geometry -- 32 bytes per lane
-// per shard (two dwordx4 4 KiB apart), one 8 KiB column range per workgroup --
-// so each coefficient's table halves are copied into VGPRs once per 8 dwords
-// of data instead of once per 2 (the shipped 8 B decode spends 99 of its ~580
-// VALU instructions per wave on those copies). Selected only by
-// hec_set_decode_vector_bytes(32), on shard lengths that are a multiple of
-// 8 KiB below 4 GiB. All four rows are computed (padded rows multiply by 0);
-// only the erased ones are stored.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void rs104_wide_kernel(ApplyArgs a) {
-    constexpr int K = 10, N = 14, R = 4, W = 8;
-    uint32_t stripe, chunk;
-    fast_item(a, a.chunks_per_stripe, stripe, chunk);
-    uint8_t* b = a.out_base + uint64_t(stripe) * a.out_stripe;  // in place (in_base == out_base)
-    const uint32_t mask = as_const(a.masks)[stripe] & ((1u << N) - 1);
-    const uint32_t present = __builtin_popcount(mask);
-    if (present < K && chunk == 0 && threadIdx.x == 0 && a.bad_count) atomicAdd(a.bad_count, 1u);
-    if (present >= K && present < N) {
-        const uint32_t nout = N - present;
-        uint32_t in_id[K], out_id[R];
-        uint32_t m = mask;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            in_id[i] = __builtin_ctz(m);
-            m &= m - 1;
-        }
-        uint32_t e = ~mask & ((1u << N) - 1);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            out_id[r] = e ? __builtin_ctz(e) : 0;
-            e &= e - 1;
-        }
-        uint32_t plan = as_const(a.lut)[mask];
-        const uint32_t o = chunk * (kThreads * 32) + threadIdx.x * 16;
-        uint32_t d[K][W];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const u32x4 lo = load_at(b + uint64_t(in_id[i]) * a.in_shard, o);
-            const u32x4 hi = load_at(b + uint64_t(in_id[i]) * a.in_shard, o + uint32_t(kThreads * 16));
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                d[i][w] = lo[w];
-                d[i][4 + w] = hi[w];
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // all twenty loads in flight before the math
-        asm volatile("" : "+s"(plan));
-        cu32p tab = as_const(a.tabs) + plan * (K * R * 5);
-        uint32_t acc[R][W];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int w = 0; w < W; ++w) acc[r][w] = 0;
-#pragma unroll
-        for (int i = 0; i < K; i += 2) {
-            // opaque per pair: its 40 table words are loaded here, not hoisted
-            // with the other pairs' (200 SGPRs, spilled)
-            uint64_t tp = reinterpret_cast<uint64_t>(tab + i * (R * 5));
-            uint32_t lo = uint32_t(tp), hi = uint32_t(tp >> 32);
-            asm volatile("" : "+s"(lo), "+s"(hi));
-            cu32p t0 = reinterpret_cast<cu32p>((uint64_t(hi) << 32) | lo), t1 = t0 + R * 5;
-            // the pair's 40 table words; the 16 halves a v_perm needs in a
-            // VGPR are copied once and reused by all 8 dwords of the lane
-            uint32_t ta[R * 5], tb[R * 5];
-#pragma unroll
-            for (int j = 0; j < R * 5; ++j) {
-                ta[j] = t0[j];
-                tb[j] = t1[j];
-            }
-            uint32_t va[R][2], vb[R][2];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                va[r][0] = ta[r * 5 + 1];
-                va[r][1] = ta[r * 5 + 3];
-                vb[r][0] = tb[r * 5 + 1];
-                vb[r][1] = tb[r * 5 + 3];
-                asm volatile("" : "+v"(va[r][0]), "+v"(va[r][1]), "+v"(vb[r][0]), "+v"(vb[r][1]));
-            }
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint32_t x0 = d[i][w], x1 = d[i + 1][w];
-                const uint32_t s00 = x0 & 0x07070707u, s01 = (x0 >> 3) & 0x07070707u, s02 = (x0 >> 6) & 0x03030303u;
-                const uint32_t s10 = x1 & 0x07070707u, s11 = (x1 >> 3) & 0x07070707u, s12 = (x1 >> 6) & 0x03030303u;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint32_t p0 = __builtin_amdgcn_perm(va[r][0], ta[r * 5 + 0], s00);
-                    const uint32_t p1 = __builtin_amdgcn_perm(va[r][1], ta[r * 5 + 2], s01);
-                    const uint32_t p2 = __builtin_amdgcn_perm(ta[r * 5 + 4], ta[r * 5 + 4], s02);
-                    const uint32_t q0 = __builtin_amdgcn_perm(vb[r][0], tb[r * 5 + 0], s10);
-                    const uint32_t q1 = __builtin_amdgcn_perm(vb[r][1], tb[r * 5 + 2], s11);
-                    const uint32_t q2 = __builtin_amdgcn_perm(tb[r * 5 + 4], tb[r * 5 + 4], s12);
-                    uint32_t x = __builtin_amdgcn_bitop3_b32(acc[r][w], p0, p1, 0x96);
-                    x = __builtin_amdgcn_bitop3_b32(x, p2, q0, 0x96);
-                    acc[r][w] = __builtin_amdgcn_bitop3_b32(x, q1, q2, 0x96);
-                }
-            }
-        }
-        // every row materialised before the uniform store branches (else the
-        // math sinks into them and the table words stay live: SGPR spills)
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int w = 0; w < W; ++w) asm volatile("" ::"v"(acc[r][w]));
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (r < int(nout)) {
-                uint8_t* sb = b + uint64_t(out_id[r]) * a.out_shard;
-                store_at(sb, o, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
-                store_at(sb, o + uint32_t(kThreads * 16), u32x4{acc[r][4], acc[r][5], acc[r][6], acc[r][7]});
-            }
-    }
-    if (a.done_flag) signal_done(a.done_count, a.done_flag, a.done_seq);
-}
-
-// ---------------------------------------------------------------------------
 // Bit-sliced RS(10,4) encode (fixed parity matrix). A lane owns 32 bytes of
 // every shard (two 16-byte vectors 4 KiB apart, so each load instruction stays
 // one contiguous 1 KiB per wave). Its 8 dwords per shard are transposed into 8
@@ -803,18 +687,18 @@ hipError_t launch_rs104_ragged(const RaggedArgs& a, bool decode, hipStream_t str
 // The kernel an aligned RS(10,4) batch with the fast plan layout runs, shared
 // by launch_apply and the name functions so a reported name is the kernel
 // that runs.
-enum class Rs104Kind { Apply, Bitslice, Narrow, Wide, Table };
-static Rs104Kind rs104_pick(uint64_t len, uint64_t n_stripes, bool dec, const LaunchConfig& cfg) {
+enum class Rs104Kind { Apply, Bitslice, Narrow, Table };
+static Rs104Kind rs104_pick(uint64_t len, uint64_t n_stripes, bool dec, bool over_pcie) {
     // launch_apply sizes its stripe ranges for 4 KiB chunks; a batch whose
     // chunks would pass one launch's workgroup limit takes the generic kernel
     const uint64_t items = (len + 4095) / 4096 * n_stripes;
     if (items > kMaxLaunchBlocks) return Rs104Kind::Apply;
     const bool off32 = len <= 0xFFFFFFFFull;
-    if (!dec && !cfg.over_pcie && len % kBsChunk == 0) return Rs104Kind::Bitslice;
-    const bool narrow = dec ? cfg.dec_vec_bytes == 8 : cfg.over_pcie;
-    if (narrow && off32 && len % kNarrowChunk == 0 && (len / kNarrowChunk) * n_stripes <= kMaxLaunchBlocks)
+    if (!dec && !over_pcie && len % kBsChunk == 0) return Rs104Kind::Bitslice;
+    // the decode, and the encode over PCIe: 8 bytes per lane where the shard
+    // length is a multiple of 2 KiB
+    if ((dec || over_pcie) && off32 && len % kNarrowChunk == 0 && (len / kNarrowChunk) * n_stripes <= kMaxLaunchBlocks)
         return Rs104Kind::Narrow;
-    if (dec && cfg.dec_vec_bytes == 32 && off32 && len % kBsChunk == 0) return Rs104Kind::Wide;
     return Rs104Kind::Table;
 }
 
@@ -825,21 +709,20 @@ static const char* rs104_name(Rs104Kind k, bool dec) {
         case Rs104Kind::Narrow:
             return dec ? "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)"
                        : "rs104_narrow_kernel<DEC=false, 8 B per lane> (table lookup)";
-        case Rs104Kind::Wide: return "rs104_wide_kernel<DEC=true, 32 B per lane> (table lookup, experiment)";
         default: return dec ? "rs104_kernel<DEC=true> (table lookup)" : "rs104_kernel<DEC=false> (table lookup)";
     }
 }
 
 constexpr const char* kNoLaunch = "none (empty shards: EmptyShard, no launch)";
 
-const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
+const char* decode_kernel_name(uint64_t len) {
     if (len == 0) return kNoLaunch;
-    return rs104_name(rs104_pick(len, 1, true, cfg), true);
+    return rs104_name(rs104_pick(len, 1, true, false), true);
 }
 
-const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg) {
+const char* encode_kernel_name(uint64_t len, bool over_pcie) {
     if (len == 0) return kNoLaunch;
-    return rs104_name(rs104_pick(len, 1, false, cfg), false);
+    return rs104_name(rs104_pick(len, 1, false, over_pcie), false);
 }
 
 // Launch constants of fast_item: the XCD eighths of the grid and the chunks
@@ -873,11 +756,6 @@ static hipError_t launch_rs104(ApplyArgs a, Rs104Kind kind, hipStream_t stream) 
             if (a.n_items == 0) return hipSuccess;
             hipLaunchKernelGGL((rs104_narrow_kernel<DEC>), dim3(uint32_t(a.n_items)), dim3(kThreads), 0, stream, a);
             break;
-        case Rs104Kind::Wide:
-            set_fast_map(a, kBsChunk, false);
-            if (a.n_items == 0) return hipSuccess;
-            hipLaunchKernelGGL(rs104_wide_kernel, dim3(uint32_t(a.n_items)), dim3(kThreads), 0, stream, a);
-            break;
         default:
             set_fast_map(a, kThreads * kVecBytes, true);
             if (a.n_items == 0) return hipSuccess;
@@ -903,8 +781,7 @@ static hipError_t launch_t(ApplyArgs a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
-                        hipStream_t stream) {
+hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, bool over_pcie, hipStream_t stream) {
     // RS(10,4) fast path: fixed 4-row table stride, one chunk of >= 2 KiB per
     // workgroup and no grid-stride loop, so one launch takes at most
     // kMaxLaunchBlocks chunks: larger batches (tens of millions of short
@@ -920,12 +797,12 @@ hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchC
             b.in_base += uint64_t(s0) * a.in_stripe;
             b.out_base += uint64_t(s0) * a.out_stripe;
             if (b.masks) b.masks += s0;
-            hipError_t e = launch_apply(b, nin, aligned, cfg, stream);
+            hipError_t e = launch_apply(b, nin, aligned, over_pcie, stream);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    const Rs104Kind kind = rs104_pick(a.len, a.n_stripes, a.masks != nullptr, cfg);
+    const Rs104Kind kind = rs104_pick(a.len, a.n_stripes, a.masks != nullptr, over_pcie && !a.masks);
     if (a.fast104 && aligned && kind != Rs104Kind::Apply)
         return a.masks ? launch_rs104<true>(a, kind, stream) : launch_rs104<false>(a, kind, stream);
     if (nin == 10) return aligned ? launch_t<10, true>(a, stream) : launch_t<10, false>(a, stream);

@@ -101,28 +101,22 @@ constexpr uint32_t kBsChunk = 2 * kThreads * kVecBytes;  // 8 KiB
 constexpr uint32_t kNarrowChunk = kThreads * 8;  // 2 KiB
 hipError_t launch_rs104_bs_ragged(const RaggedArgs& a, hipStream_t stream);
 
-struct LaunchConfig {
-    int dec_vec_bytes = 8;   // RS(10,4) device decode bytes per lane per shard: 8 (default: dwordx2, 2 KiB
-                             // per workgroup, on shard lengths a multiple of 2 KiB; others take 16),
-                             // 16, or 32 (the round-6 experiment, rs104_wide_kernel; speed only)
-    bool over_pcie = false;  // set by the zero-copy host encodes (the kernel streams host memory over
-                             // PCIe): the 8-byte-per-lane table encode where the shard length is a
-                             // multiple of 2 KiB instead of the bit-sliced one (its narrower column range
-                             // per workgroup ran 50.5-52.9 against 49.4-51.1 GiB/s in 7 alternating
-                             // rounds on two boxes, profiles/r04/e2e_encode_kernels_{v,w}.jsonl)
-};
 
-// Launch one coding pass. k_fixed: number of inputs the caller guarantees
-// (10 selects the unrolled helyim RS(10,4) path; anything else the generic loop).
-hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, const LaunchConfig& cfg,
-                        hipStream_t stream);
+// Launch one coding pass. nin: number of inputs the caller guarantees (10
+// selects the unrolled helyim RS(10,4) path; anything else the generic loop).
+// over_pcie: an encode whose operands are host memory the kernel streams over
+// PCIe (zero-copy host batches): the 8-byte-per-lane table encode where the
+// shard length is a multiple of 2 KiB instead of the bit-sliced one (its
+// narrower column range per workgroup ran 50.5-52.9 against 49.4-51.1 GiB/s
+// in 7 alternating rounds on two boxes, profiles/r04/e2e_encode_kernels_{v,w}.jsonl).
+hipError_t launch_apply(const ApplyArgs& a, int nin, bool aligned, bool over_pcie, hipStream_t stream);
 
 // Name of the kernel an aligned RS(10,4) device encode of one stripe of this
 // shard length runs under cfg (introspection for benchmarks and profiles; the
 // same choice launch_apply makes, rs_kernels.hip rs104_pick).
-const char* encode_kernel_name(uint64_t len, const LaunchConfig& cfg);
+const char* encode_kernel_name(uint64_t len, bool over_pcie);
 // Same for an aligned in-place RS(10,4) device batch reconstruct.
-const char* decode_kernel_name(uint64_t len, const LaunchConfig& cfg);
+const char* decode_kernel_name(uint64_t len);
 
 // splitmix64 byte stream per stripe (bench/test data generator):
 // stripe s: bytes_per_stripe bytes at base + s*stripe_stride, word n (n>=1) =

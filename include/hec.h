@@ -402,12 +402,9 @@ int hec_ec_volume_read_needles(hec_ec_volume_t* vol, const uint64_t* needle_ids,
                                uint64_t* out_offsets, int* statuses);
 
 /* ---- tuning / introspection ----------------------------------------------- */
-/* RS(10,4) device decode bytes per lane per shard (process-wide; speed only,
- * results identical): 8 (default; 2 KiB per workgroup, on shard lengths that
- * are a multiple of 2 KiB, others take 16), 16 (4 KiB per workgroup), or 32
- * (the round-6 experiment: 8 KiB per workgroup, on shard lengths that are a
- * multiple of 8 KiB). HEC_ERR_INVALID_ARGUMENT otherwise. */
-int hec_set_decode_vector_bytes(int bytes);
+/* Kernel choice has no knob: it follows the shard length, the alignment and
+ * where the bytes live (hec_*_kernel_name below report it). The knobs left
+ * (process-wide, results identical) are the host paths' thresholds and mode. */
 /* Host-memory encode / reconstruct calls whose input (data shards x shard
  * length) is at most max_bytes are packed into pinned staging and moved with
  * one H2D and one D2H copy; larger calls copy each shard directly. 0 disables

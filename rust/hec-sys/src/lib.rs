@@ -186,7 +186,6 @@ extern "C" {
                                       cap: usize, out_offsets: *mut u64, statuses: *mut c_int) -> c_int;
 
     // tuning / introspection (speed only)
-    pub fn hec_set_decode_vector_bytes(bytes: c_int) -> c_int;
     pub fn hec_set_host_staging(max_bytes: u64) -> c_int;
     pub fn hec_set_completion_signal(max_bytes: u64) -> c_int;
     pub fn hec_set_host_zero_copy(on: c_int) -> c_int;

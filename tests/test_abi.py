@@ -236,26 +236,15 @@ def test_strided_batch_geometry_checked_before_device():
 
 def test_decode_kernel_name_follows_dispatch():
     """hec_decode_kernel_name comes from the same choice the launcher makes
-    (rs104_pick): 8 B per lane on multiples of 2 KiB (default), the 16-byte
-    table kernel otherwise or under hec_set_decode_vector_bytes(16), the
-    round-6 32 B experiment only on multiples of 8 KiB; other widths refused."""
+    (rs104_pick): 8 B per lane on multiples of 2 KiB, the 16-byte table kernel
+    on other 16-byte multiples; there is no width knob (round 6)."""
     import helyim_amd as H
     lib = H.lib
-    try:
-        assert lib.hec_decode_kernel_name(1 << 20).decode() == "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)"
-        assert lib.hec_decode_kernel_name(2048).decode().startswith("rs104_narrow_kernel<DEC=true")
-        assert lib.hec_decode_kernel_name(2048 + 16).decode().startswith("rs104_kernel<DEC=true>")
-        for bad in (0, 4, 12, 64):
-            assert lib.hec_set_decode_vector_bytes(bad) == 66
-        assert lib.hec_set_decode_vector_bytes(16) == 0
-        assert lib.hec_decode_kernel_name(1 << 20).decode().startswith("rs104_kernel<DEC=true>")
-        assert lib.hec_set_decode_vector_bytes(32) == 0
-        assert lib.hec_decode_kernel_name(1 << 20).decode().startswith("rs104_wide_kernel<DEC=true, 32 B per lane>")
-        assert lib.hec_decode_kernel_name(2048).decode().startswith("rs104_kernel<DEC=true>")
-        # the encode never takes the decode's width
-        assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced)"
-    finally:
-        lib.hec_set_decode_vector_bytes(8)
+    assert lib.hec_decode_kernel_name(1 << 20).decode() == "rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)"
+    assert lib.hec_decode_kernel_name(2048).decode().startswith("rs104_narrow_kernel<DEC=true")
+    assert lib.hec_decode_kernel_name(2048 + 16).decode().startswith("rs104_kernel<DEC=true>")
+    assert not hasattr(lib, "hec_set_decode_vector_bytes")
+    assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced)"
 
 
 def test_ragged_kernel_name_follows_the_launch_choice():

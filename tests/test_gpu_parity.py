@@ -341,38 +341,6 @@ def test_batch_encode_vs_oracle(gpu, L):
     assert np.array_equal(host[:, 10:], ref)
 
 
-@pytest.mark.parametrize("dv", [8, 16, 32])
-def test_decode_widths_identical(gpu, dv):
-    """Every decode width (hec_set_decode_vector_bytes 8: the shipped 2 KiB
-    column range; 16: 4 KiB; 32: the round-6 experiment's 8 KiB) gives the
-    default's bytes on random 0-4 erasure patterns, at a length every width
-    takes and at one only the 16-byte kernel takes."""
-    import torch
-    import helyim_amd as H
-    import helyim_amd.batch as B
-    rs = H.ReedSolomon(10, 4)
-    for S, L in ((37, 3 * 8192), (29, 3 * 8192 + 48)):
-        t = _stripes(S, L)
-        B.encode_batch(rs, t)
-        ref = t.clone()
-        rng = np.random.default_rng(dv * 1000 + L)
-        masks = np.array([((1 << 14) - 1) & ~int(sum(1 << int(i) for i in rng.choice(14, int(rng.integers(0, 5)),
-                                                                                     replace=False)))
-                          for _ in range(S)], dtype=np.int32)
-        er = torch.from_numpy(((masks[:, None] >> np.arange(14)[None, :]) & 1) == 0).cuda()
-        t[er] = 0x5A
-        try:
-            assert H.lib.hec_set_decode_vector_bytes(dv) == 0
-            name = H.lib.hec_decode_kernel_name(L).decode()
-            assert ("32 B per lane" in name) == (dv == 32 and L % 8192 == 0), name
-            assert ("8 B per lane" in name) == (dv == 8 and L % 2048 == 0), name
-            B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda())
-            torch.cuda.synchronize()
-        finally:
-            H.lib.hec_set_decode_vector_bytes(8)
-        assert torch.equal(t, ref), (dv, L)
-
-
 def test_bitslice_encode_matches_oracle(gpu):
     """The encode kernels against the C oracle: lengths that are a multiple of
     8 KiB take the bit-sliced kernel, other 16-byte multiples the table
@@ -445,15 +413,14 @@ def test_batch_reconstruct_every_pattern(gpu):
     assert torch.equal(t, good)
 
 
-@pytest.mark.parametrize("vec", [16, 8, 32])
-@pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192 + 16, 2048 * 5])
-def test_decode_kernels_every_pattern(gpu, vec, L):
-    """The RS(10,4) decode kernels (16 bytes per lane over one 4 KiB chunk per
-    workgroup, 8 bytes per lane over 2 KiB -- the default --, and the round-6
-    32-byte experiment over 8 KiB) with all loads issued before the math: all
+@pytest.mark.parametrize("L", [8192, 3 * 8192, 8 * 8192 + 16, 2048 * 5, 4096 + 48])
+def test_decode_kernels_every_pattern(gpu, L):
+    """The RS(10,4) decode kernels -- 8 bytes per lane over 2 KiB column
+    ranges where the shard length is a multiple of 2 KiB, 16 bytes per lane
+    over 4 KiB otherwise -- with all ten loads issued before the math: all
     1470 patterns (erased slots poisoned), plus an all-present stripe (no-op)
     and two with too few present (skipped, counted), vs the originals; the
-    kernel-name report follows the width and the length."""
+    kernel-name report follows the length."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
@@ -470,16 +437,12 @@ def test_decode_kernels_every_pattern(gpu, vec, L):
             masks[s] &= ~(1 << i)
     masks[-2] = (1 << 14) - 1 - 0b11111           # 9 present
     masks[-1] = (1 << 14) - 1 - (0b1111 << 10) - 1  # 9 present, all parity gone
-    try:
-        assert H.lib.hec_set_decode_vector_bytes(vec) == 0
-        name = H.lib.hec_decode_kernel_name(L).decode()
-        assert ("8 B per lane" in name) == (vec == 8 and L % 2048 == 0), name
-        assert ("32 B per lane" in name) == (vec == 32 and L % 8192 == 0), name
-        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
-        B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda(), bad)
-        torch.cuda.synchronize()
-    finally:
-        H.lib.hec_set_decode_vector_bytes(8)
+    name = H.lib.hec_decode_kernel_name(L).decode()
+    assert ("8 B per lane" in name) == (L % 2048 == 0), name
+    assert name.startswith("rs104_narrow_kernel<DEC=true" if L % 2048 == 0 else "rs104_kernel<DEC=true>"), name
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.reconstruct_batch(rs, t, torch.from_numpy(masks).cuda(), bad)
+    torch.cuda.synchronize()
     assert int(bad.item()) == 2
     assert torch.equal(t, good)
 
@@ -909,53 +872,47 @@ def test_device_batches_generic_geometry(gpu, k, m):
 def test_randomised_device_batches_vs_oracle(gpu):
     """Seeded sweep over the device batch API: shard lengths (tiny, odd,
     16-byte and 8 KiB multiples), shard pitches (tight, padded, unaligned),
-    in-place and separate parity buffers, per-stripe erasure patterns, and
-    every decode width (8, 16 and the 32-byte experiment), all against the C
-    oracle."""
+    in-place and separate parity buffers and per-stripe erasure patterns, all
+    against the C oracle."""
     import torch
     import helyim_amd as H
     import helyim_amd.batch as B
     rng = np.random.default_rng(20261016)
     rs = H.ReedSolomon(10, 4)
-    lib = H.lib
     lens = [1, 15, 16, 17, 100, 4080, 4096, 4112, 8192, 12288, 16384, 24576, 65536, 65536 + 48, 100003]
-    try:
-        for case in range(120):
-            L = int(rng.choice(lens))
-            S = int(rng.integers(1, 9))
-            pad = int(rng.choice([0, 16, 48, 4096, 3]))
-            sep = bool(rng.integers(0, 2))
-            assert lib.hec_set_decode_vector_bytes(int(rng.choice([8, 16, 32]))) == 0
-            P = L + pad
-            raw = torch.zeros(S * 14 * P + 16, dtype=torch.uint8, device="cuda")
-            t = raw[:S * 14 * P].view(S, 14, P)[:, :, :L]
-            host = np.zeros((S, 14, L), np.uint8)
-            host[:, :10] = rng.integers(0, 256, (S, 10, L), dtype=np.uint8)
-            host[:, 10:] = corc.encode_stripes(np.ascontiguousarray(host[:, :10]))
-            t[:, :10] = torch.from_numpy(host[:, :10]).cuda()
-            if sep:
-                par_raw = torch.zeros(S * 4 * P + 16, dtype=torch.uint8, device="cuda")
-                par = par_raw[:S * 4 * P].view(S, 4, P)[:, :, :L]
-                B.encode_batch_sep(rs, t[:, :10], par)
-                torch.cuda.synchronize()
-                assert np.array_equal(par.cpu().numpy(), host[:, 10:]), (case, L, S, pad)
-                t[:, 10:] = par
-            else:
-                B.encode_batch(rs, t)
-                torch.cuda.synchronize()
-                assert np.array_equal(t.cpu().numpy(), host), (case, L, S, pad)
-            masks = np.full(S, 0x3FFF, np.int64)
-            for s in range(S):
-                for i in rng.choice(14, int(rng.integers(0, 5)), replace=False):
-                    masks[s] &= ~(1 << int(i))
-                    t[s, int(i)] = 0xEE
-            bad = torch.zeros(1, dtype=torch.int32, device="cuda")
-            B.reconstruct_batch(rs, t, torch.from_numpy(masks.astype(np.int32)).cuda(), bad)
+    for case in range(120):
+        L = int(rng.choice(lens))
+        S = int(rng.integers(1, 9))
+        pad = int(rng.choice([0, 16, 48, 4096, 3]))
+        sep = bool(rng.integers(0, 2))
+        P = L + pad
+        raw = torch.zeros(S * 14 * P + 16, dtype=torch.uint8, device="cuda")
+        t = raw[:S * 14 * P].view(S, 14, P)[:, :, :L]
+        host = np.zeros((S, 14, L), np.uint8)
+        host[:, :10] = rng.integers(0, 256, (S, 10, L), dtype=np.uint8)
+        host[:, 10:] = corc.encode_stripes(np.ascontiguousarray(host[:, :10]))
+        t[:, :10] = torch.from_numpy(host[:, :10]).cuda()
+        if sep:
+            par_raw = torch.zeros(S * 4 * P + 16, dtype=torch.uint8, device="cuda")
+            par = par_raw[:S * 4 * P].view(S, 4, P)[:, :, :L]
+            B.encode_batch_sep(rs, t[:, :10], par)
             torch.cuda.synchronize()
-            assert int(bad.item()) == 0
-            assert np.array_equal(t.cpu().numpy(), host), (case, L, S, pad, "decode")
-    finally:
-        lib.hec_set_decode_vector_bytes(8)
+            assert np.array_equal(par.cpu().numpy(), host[:, 10:]), (case, L, S, pad)
+            t[:, 10:] = par
+        else:
+            B.encode_batch(rs, t)
+            torch.cuda.synchronize()
+            assert np.array_equal(t.cpu().numpy(), host), (case, L, S, pad)
+        masks = np.full(S, 0x3FFF, np.int64)
+        for s in range(S):
+            for i in rng.choice(14, int(rng.integers(0, 5)), replace=False):
+                masks[s] &= ~(1 << int(i))
+                t[s, int(i)] = 0xEE
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        B.reconstruct_batch(rs, t, torch.from_numpy(masks.astype(np.int32)).cuda(), bad)
+        torch.cuda.synchronize()
+        assert int(bad.item()) == 0
+        assert np.array_equal(t.cpu().numpy(), host), (case, L, S, pad, "decode")
 
 
 def test_randomised_ragged_batches_vs_oracle(gpu):

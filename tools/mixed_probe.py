@@ -37,7 +37,6 @@ def main():
     ap.add_argument("--fixed-e", type=int, default=-1,
                     help=">= 0: every stripe exactly this many erasures, lengths still mixed (separates the e mix)")
     ap.add_argument("--pads", default="0", help="gap after every shard, one layout per value")
-    ap.add_argument("--decvecs", default="8", help="decode bytes per lane (hec_set_decode_vector_bytes), per round")
     ap.add_argument("--orders", default="given",
                     help="descriptor order of the ragged calls, per round: given (stripe order) or dealt "
                          "(each erasure count's stripes split into 8 parts of equal workgroup counts, part x of "
@@ -125,10 +124,8 @@ def main():
     st = torch.cuda.current_stream()
     kinds = ["ragged"] + (["strided"] if args.strided and (args.uniform or args.fixed_len) else [])
     mask_t = torch.tensor(masks, dtype=torch.int32, device="cuda")
-    for r, p, dv, er, kind, order in ((r, p, int(dv), int(er), k, o) for r in range(args.rounds) for p in pads
-                                      for dv in args.decvecs.split(",") for er in ("1",)
-                                      for k in kinds for o in (orders if k == "ragged" else ["given"])):
-        H.lib.hec_set_decode_vector_bytes(dv)
+    for r, p, kind, order in ((r, p, k, o) for r in range(args.rounds) for p in pads
+                              for k in kinds for o in (orders if k == "ragged" else ["given"])):
         descs = lays[p][0]
         L0 = int(Ls[0])
         view = dev.as_strided((n, 14, L0), (14 * (L0 + p), L0 + p, 1))
@@ -155,14 +152,13 @@ def main():
         dec_b = sum((14 - bin(d[3]).count("1") + 10) * d[2] for d in descs if d[3] != full)
         print(json.dumps({"lib": os.path.basename(H.LIB_PATH), "uniform": args.uniform, "stripes": n,
                           "fixed_len": args.fixed_len, "fixed_e": args.fixed_e,
-                          "kind": kind, "order": order, "pad": p, "dec_vec_bytes": dv, "enc_remap": er,
+                          "kind": kind, "order": order, "pad": p,
                           "round": r,
                           "enc_TBps": round(enc_b / enc / 1e9, 3), "dec_TBps": round(dec_b / dec / 1e9, 3),
                           "GiB_s": round(payload / (wall * 1e-3) / 2**30, 1),
                           "ms_per_rep": round(wall, 3), "enc_ms": round(float(enc), 3),
                           "dec_ms": round(float(dec), 3), "payload_GiB": round(payload / 2**30, 3),
                           "enc_bytes": int(enc_b), "dec_bytes": int(dec_b)}), flush=True)
-    H.lib.hec_set_decode_vector_bytes(8)
     descs = lays[pads[0]][0]
     if args.grouped:
         del dev

@@ -15,6 +15,9 @@ import statistics
 import sys
 
 SIMDS = 256 * 4
+# input bytes one launch reads (the BASELINE batch: 4096 stripes x 10 x 1 MiB);
+# set to 0 to leave valu_insts_per_KiB out for other workloads
+BYTES_PER_LAUNCH = 4096 * 10 * (1 << 20)
 
 
 def main():
@@ -26,12 +29,14 @@ def main():
         per[key][r["Counter_Name"]] += float(r["Counter_Value"])
         meta[key] = (r["Kernel_Name"], int(r["Grid_Size"]),
                      (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6, int(r["VGPR_Count"]))
-    big = max(g for _, g, _, _ in meta.values())
+    big = collections.defaultdict(int)  # largest grid per kernel: the batch-size dispatches
+    for name, g, _, _ in meta.values():
+        big[name] = max(big[name], g)
     out = {"source": src, "units": __doc__.split("Units")[1].split("usage")[0].strip(), "kernels": {}}
     by_kernel = collections.defaultdict(list)
     for key, c in per.items():
         name, grid, ms, vgpr = meta[key]
-        if grid * 2 < big and "bs_encode" not in name:  # skip the small verification dispatches
+        if grid * 2 < big[name]:  # skip the small verification dispatches
             continue
         cycles = c["GRBM_GUI_ACTIVE"] / 8
         wc = c["SQ_WAVE_CYCLES"]
@@ -43,6 +48,7 @@ def main():
             "wave_issue_stalled": c["SQ_WAIT_INST_ANY"] / wc,
             "wave_issuing": c["SQ_ACTIVE_INST_ANY"] / wc,
             "valu_insts_per_wave": c["SQ_INSTS_VALU"] / c["SQ_WAVES"],
+            "valu_insts_per_KiB": c["SQ_INSTS_VALU"] * 1024 / BYTES_PER_LAUNCH if BYTES_PER_LAUNCH else None,
         })
     for name, ds in by_kernel.items():
         ds = ds[1:] if len(ds) > 1 else ds  # first dispatch is the warm-up

@@ -210,7 +210,7 @@ def host_zero_copy(t: torch.Tensor) -> bool:
 
 def ragged_kernel_name(descs, decode: bool) -> str:
     """The kernel (and workgroup order) encode_ragged / reconstruct_ragged runs
-    on these descriptors under the current knobs (hec_ragged_kernel_name: the
+    on these descriptors (hec_ragged_kernel_name: the
     launch's own choice)."""
     import numpy as np
     d = descs if isinstance(descs, np.ndarray) and descs.dtype == desc_dtype() else \

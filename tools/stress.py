@@ -168,21 +168,21 @@ def main():
         assert np.array_equal(dec, enc), "device_ragged reconstruct"
         note("device_ragged")
 
-    def knobs(rng):
+    def census(rng):
         # the staging census while other threads' host batches are in flight
         # (it must not stall their leases)
         import ctypes
         n, pin, dev = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
         assert H.lib.hec_host_staging_stats(ctypes.byref(n), ctypes.byref(pin), ctypes.byref(dev)) == 0
         assert 0 <= n.value <= 8, n.value
-        note("knobs")
+        note("census")
 
     def worker(t_id):
         rng = np.random.default_rng(1000 + t_id)
         torch.cuda.set_device(0)
         stream = torch.cuda.Stream()
         ops = [percall, host_batch, ragged, lambda r: files(r, t_id), lambda r: device(r, stream),
-               lambda r: device_ragged(r, stream), knobs]
+               lambda r: device_ragged(r, stream), census]
         while time.monotonic() < stop:
             op = ops[int(rng.integers(0, len(ops)))]
             try:

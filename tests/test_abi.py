@@ -30,6 +30,22 @@ def test_library_loads_and_exports_header():
     assert "gfx950" in helyim_amd.version()
 
 
+def test_speed_settings_are_the_three_host_path_knobs():
+    """hec.h keeps only settings whose non-default value a
+    product path uses (the host paths' staging threshold, zero copy or SDMA
+    copies, completion-flag threshold); kernel choice has no knob, and the
+    removed measurement switches are gone from the library too."""
+    import helyim_amd
+    setters = [n for n in declared_functions() if n.startswith("hec_set_")]
+    assert sorted(setters) == ["hec_set_completion_signal", "hec_set_device", "hec_set_host_staging",
+                               "hec_set_host_zero_copy"]
+    for gone in ("hec_set_launch_config", "hec_set_kernel_mode", "hec_set_workgroup_size",
+                 "hec_set_decode_vector_bytes", "hec_set_encode_vector_bytes", "hec_set_encode_kernel",
+                 "hec_set_bitslice_vector_bytes", "hec_set_ragged_encode_remap", "hec_set_host_encode_narrow",
+                 "hec_set_xcd_parts", "hec_set_chunk_rotation", "hec_set_file_zero_copy", "hec_file_path_stats"):
+        assert not hasattr(helyim_amd.lib, gone), gone
+
+
 def test_library_is_gfx950_code_object():
     so = os.path.join(ROOT, "helyim_amd", "libhec.so")
     blob = open(so, "rb").read()

@@ -77,6 +77,11 @@ def test_rebuild_errors(gpu, tmp_path):
     with pytest.raises(H.ErasureCoding) as ei:
         H.rebuild_ec_files(base)
     assert isinstance(ei.value.inner, H.TooFewShardsPresent)
+    # the missing shards' outputs were created and truncated before decoding,
+    # so the failed rebuild leaves them empty, as the reference's does
+    # (encoder.rs:96-104 opens them before rebuild_ec_files_inner)
+    for i in range(5):
+        assert os.path.getsize(base + H.to_ext(i)) == 0, i
     for i in range(5):
         os.replace(base + H.to_ext(i) + ".bak", base + H.to_ext(i))
     # shard 0 one row + 5 bytes long: the second row reads n = 5 != 1 MiB ->

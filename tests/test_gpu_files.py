@@ -64,6 +64,32 @@ def test_unexpected_block_size(gpu, tmp_path):
     assert str(ei.value) == "unexpected block size 32, buffer size 24"
 
 
+@pytest.mark.parametrize("buf,large,small,size,written", [
+    (16, 640, 24, 6400 + 1000, 640),  # one large row coded, then the small rows' check fails
+    (24, 640, 32, 6400 + 1000, 0),    # the first large row's check fails: nothing coded
+])
+def test_unexpected_block_size_leaves_the_reference_bytes(gpu, tmp_path, buf, large, small, size, written):
+    """UnexpectedBlockSize is raised by encode_data at the first row of a kind
+    whose block the buffer does not divide (encoder.rs:139-144), after the
+    rows before it were written: the 14 files hold exactly those rows, byte
+    for byte the oracle's encoder.rs restatement, which stops at the same
+    point."""
+    import helyim_amd as H
+    dat = O.splitmix64_bytes(77, size).tobytes()
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    for base in (a, b):
+        open(base + ".dat", "wb").write(dat)
+    with pytest.raises(H.UnexpectedBlockSize) as ei:
+        H.generate_ec_files(a, buf, large, small)
+    with pytest.raises(O.UnexpectedBlockSize):
+        O.write_ec_files(b, buf, large, small)
+    assert (ei.value.block_size, ei.value.buf_size) == ((small if written else large), buf)
+    for i in range(14):
+        got = open(a + H.to_ext(i), "rb").read()
+        assert len(got) == written, (i, len(got))
+        assert got == open(b + O.to_ext(i), "rb").read(), i
+
+
 def test_rebuild_errors(gpu, tmp_path):
     import helyim_amd as H
     base = str(tmp_path / "v")
@@ -172,12 +198,14 @@ def test_rebuild_stops_when_a_present_shard_ends_a_row_early(gpu, tmp_path, shor
         assert got[i] == sh[i][: 1 << 20].tobytes()
 
 
-def test_rebuild_over_all_empty_present_shards(gpu, tmp_path):
+@pytest.mark.parametrize("lost", [[0, 7, 10, 13], list(range(5, 14))])
+def test_rebuild_over_all_empty_present_shards(gpu, tmp_path, lost):
     """Every present shard empty: the first read returns 0 bytes at offset 0
     (encoder.rs:269-271), so rebuild_ec_files returns the missing ids with
-    their files created (open with create + truncate: :96-103) and empty."""
+    their files created (open with create + truncate: :96-103) and empty --
+    even with only 5 present, since the loop returns Ok before reconstruct
+    could report TooFewShardsPresent (:288)."""
     import helyim_amd as H
-    lost = [0, 7, 10, 13]
     bases = [str(tmp_path / n) for n in ("a", "b")]
     for base in bases:
         for i in range(14):
@@ -186,6 +214,21 @@ def test_rebuild_over_all_empty_present_shards(gpu, tmp_path):
     assert H.rebuild_ec_files(bases[0]) == lost
     assert O.rebuild_ec_files(bases[1]) == lost
     assert _tree(bases[0]) == _tree(bases[1]) == {i: b"" for i in range(14)}
+
+
+def test_rebuild_with_every_shard_missing(gpu, tmp_path):
+    """No shard file present: nothing is read, so the first row goes straight
+    to reconstruct with 0 present shards -> ErasureCoding(TooFewShardsPresent)
+    (encoder.rs:262-288), after all 14 outputs were created empty (:96-103)."""
+    import helyim_amd as H
+    base = str(tmp_path / "none")
+    with pytest.raises(H.ErasureCoding) as ei:
+        H.rebuild_ec_files(base)
+    assert isinstance(ei.value.inner, H.TooFewShardsPresent)
+    with pytest.raises(O.TooFewShardsPresent):
+        O.rebuild_ec_files(str(tmp_path / "none_oracle"))
+    assert _tree(base) == {i: b"" for i in range(14)}
+    assert _tree(str(tmp_path / "none_oracle")) == {i: b"" for i in range(14)}
 
 
 def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path):

@@ -249,6 +249,86 @@ def test_c_oracle_file_layer_small_geometry(tmp_path, size):
         assert open(a + O.to_ext(i), "rb").read() == open(b + O.to_ext(i), "rb").read()
 
 
+# ---- the reference's file-layer edge cases, both restatements ---------------
+def _files(base):
+    return {i: open(base + O.to_ext(i), "rb").read() for i in range(14) if os.path.exists(base + O.to_ext(i))}
+
+
+def test_oracles_zero_byte_dat(tmp_path):
+    """encoder.rs:62 remaining = 0: no row loop runs (:215, :228); the 14
+    files open_ec_files created and truncated (:111-127) stay empty."""
+    for k, write in enumerate((lambda b: O.write_ec_files(b), lambda b: corc.write_ec_files(b))):
+        base = str(tmp_path / f"z{k}")
+        open(base + ".dat", "wb").close()
+        open(base + O.to_ext(4), "wb").write(b"stale")
+        assert write(base) in (None, 0)
+        assert _files(base) == {i: b"" for i in range(14)}
+
+
+@pytest.mark.parametrize("buf,large,small,written", [(16, 640, 24, 640), (24, 640, 32, 0)])
+def test_oracles_block_size_error_after_written_rows(tmp_path, buf, large, small, written):
+    """encode_data checks block % buf at each row (encoder.rs:139-144), after
+    the rows before it were written: the files hold exactly those rows."""
+    dat = O.splitmix64_bytes(77, 7400).tobytes()
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    for base in (a, b):
+        open(base + ".dat", "wb").write(dat)
+    with pytest.raises(O.UnexpectedBlockSize) as ei:
+        O.write_ec_files(a, buf, large, small)
+    assert ei.value.args == ((small if written else large), buf)
+    assert corc.write_ec_files(b, buf, large, small) == -2
+    fa, fb = _files(a), _files(b)
+    assert fa == fb and all(len(v) == written for v in fa.values())
+
+
+@pytest.mark.parametrize("short", [0, 6, 13])
+def test_oracles_rebuild_stops_at_a_short_present_shard(tmp_path, short):
+    """rebuild_ec_files_inner returns Ok at the first present shard whose
+    read is 0 bytes (encoder.rs:268-271), before the size check (:275) and
+    before the row is reconstructed or written."""
+    L = 2 << 20
+    rs = O.ReedSolomon(10, 4)
+    sh = [O.splitmix64_bytes(700 + i, L) for i in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+    rs.encode(sh)
+    lost = [2, 11] if short not in (2, 11) else [3, 10]
+    bases = [str(tmp_path / n) for n in ("a", "b")]
+    for base in bases:
+        for i in range(14):
+            open(base + O.to_ext(i), "wb").write(sh[i].tobytes())
+        os.truncate(base + O.to_ext(short), 1 << 20)
+        for i in lost:
+            os.remove(base + O.to_ext(i))
+    assert O.rebuild_ec_files(bases[0]) == lost
+    assert corc.rebuild_ec_files(bases[1]) == (0, lost)
+    fa, fb = _files(bases[0]), _files(bases[1])
+    assert fa == fb
+    for i in lost:
+        assert fa[i] == sh[i][: 1 << 20].tobytes()
+
+
+@pytest.mark.parametrize("present", [10, 5, 0])
+def test_oracles_rebuild_over_empty_or_no_shards(tmp_path, present):
+    """Empty present shards: the first read is 0 bytes, so the rebuild
+    returns the missing ids with empty outputs -- also with only 5 present
+    (Ok comes before reconstruct's TooFewShardsPresent, encoder.rs:269-271 vs
+    :288). No shard at all: nothing is read, reconstruct reports
+    TooFewShardsPresent, all 14 outputs created empty (:96-103)."""
+    bases = [str(tmp_path / n) for n in ("a", "b")]
+    lost = list(range(present, 14))
+    for base in bases:
+        for i in range(present):
+            open(base + O.to_ext(i), "wb").close()
+    if present:
+        assert O.rebuild_ec_files(bases[0]) == lost
+        assert corc.rebuild_ec_files(bases[1]) == (0, lost)
+    else:
+        with pytest.raises(O.TooFewShardsPresent):
+            O.rebuild_ec_files(bases[0])
+        assert corc.rebuild_ec_files(bases[1])[0] == -4
+    for base in bases:
+        assert _files(base) == {i: b"" for i in range(14)}
+
+
 # ---- a third formulation: polynomial interpolation over GF(2^8) -------------
 # The construction V x inv(V[0..k]) with V[r][c] = r^c (SURVEY Appendix B) is
 # the systematic evaluation code: shard r of a stripe is p(r) for the unique

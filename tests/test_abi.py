@@ -263,6 +263,27 @@ def test_decode_kernel_name_follows_dispatch():
     assert lib.hec_encode_kernel_name(1 << 20).decode() == "rs104_bs_encode_kernel (bit-sliced)"
 
 
+def test_kernel_choice_rule_over_many_lengths():
+    """The documented rule over a sweep of 16-byte-multiple
+    shard lengths: device encode bit-sliced iff L % 8 KiB == 0, else the
+    16-byte table kernel; zero-copy host encode and device decode 8 B per
+    lane iff L % 2 KiB == 0, else the 16-byte table kernel."""
+    import helyim_amd as H
+    lib = H.lib
+    lens = sorted({16 * i for i in range(1, 600, 7)} | {2048 * i for i in range(1, 40)} |
+                  {8192 * i + d for i in range(1, 20) for d in (0, 16, 2048)} | {1 << 20, (1 << 20) + 16, 1 << 30})
+    for L in lens:
+        enc = lib.hec_encode_kernel_name(L).decode()
+        hst = lib.hec_host_encode_kernel_name(L).decode()
+        dec = lib.hec_decode_kernel_name(L).decode()
+        assert enc == ("rs104_bs_encode_kernel (bit-sliced)" if L % 8192 == 0
+                       else "rs104_kernel<DEC=false> (table lookup)"), (L, enc)
+        assert hst == ("rs104_narrow_kernel<DEC=false, 8 B per lane> (table lookup)" if L % 2048 == 0
+                       else "rs104_kernel<DEC=false> (table lookup)"), (L, hst)
+        assert dec == ("rs104_narrow_kernel<DEC=true, 8 B per lane> (table lookup)" if L % 2048 == 0
+                       else "rs104_kernel<DEC=true> (table lookup)"), (L, dec)
+
+
 def test_ragged_kernel_name_follows_the_launch_choice():
     """hec_ragged_kernel_name comes from the ragged launch's own pick
     (ragged_pick in intervals.cpp): bit-sliced only when every length is a

@@ -35,25 +35,17 @@ build/membench_calib: tools/membench.hip include/hec.h helyim_amd/libhec.so
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -DMEMBENCH_WITH_HEC -o $@ $< -Lhelyim_amd -lhec \
 	    -Wl,-rpath,'$$ORIGIN/../helyim_amd'
 
-# Measurement variants of the kernel file (cache policy of shard streams).
-VARIANTS := ntl0_nts0 ntl0_nts1 ntl1_nts0 null lf0 s_sc1 s_sc0sc1 s_sc0sc1nt s_bufnt l_bufnt
+# A/B method check: a byte-identical rebuild of the kernel file as a separate
+# library (HEC_LIB_PATH=build/variants/libhec_null.so), to measure the spread
+# of alternating-process A/Bs between two library builds (tools/tune.py).
+VARIANTS := null
 variants: $(foreach v,$(VARIANTS),build/variants/libhec_$(v).so)
 build/variants/libhec_%.so: $(SRC) $(HDR)
 	@mkdir -p build/variants/$*
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS_$*) -c helyim_amd/csrc/rs_kernels.hip -o build/variants/$*/rs_kernels.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ build/variants/$*/rs_kernels.o \
 	    $(filter-out build/obj/rs_kernels.hip.o,$(OBJ)) -lpthread
-VFLAGS_ntl0_nts0 := -DHEC_NT_LOAD=0 -DHEC_NT_STORE=0
-VFLAGS_ntl0_nts1 := -DHEC_NT_LOAD=0 -DHEC_NT_STORE=1
-VFLAGS_ntl1_nts0 := -DHEC_NT_LOAD=1 -DHEC_NT_STORE=0
 VFLAGS_null := -DHEC_NULL_VARIANT=1  # identical code: measures the A/B method itself
-VFLAGS_lf0 := -DHEC_LOADS_FIRST=0  # table kernels: loads interleaved with the math by the scheduler
-# shard stream cache policy through raw buffer instructions (gfx950 cpol: 1 sc0, 2 nt, 16 sc1)
-VFLAGS_s_sc1 := -DHEC_STORE_CPOL=16
-VFLAGS_s_sc0sc1 := -DHEC_STORE_CPOL=17
-VFLAGS_s_sc0sc1nt := -DHEC_STORE_CPOL=19
-VFLAGS_s_bufnt := -DHEC_STORE_CPOL=2
-VFLAGS_l_bufnt := -DHEC_LOAD_CPOL=2
 
 clean:
 	rm -rf build helyim_amd/libhec.so

@@ -48,89 +48,41 @@ __device__ __forceinline__ const __attribute__((address_space(4))) T* as_const(c
 }
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
-// Cache policy of the streamed shard bytes (each is touched exactly once).
-// Build-time switches for measurement variants (Makefile VARIANTS).
-#ifndef HEC_NT_LOAD
-#define HEC_NT_LOAD 1
-#endif
-#ifndef HEC_NT_STORE
-#define HEC_NT_STORE 1
-#endif
-// Table kernels: 1 = all ten shard loads issued before the math (the shipped
-// form); 0 = the scheduler's interleaving (measurement variant `lf0`).
-#ifndef HEC_LOADS_FIRST
-#define HEC_LOADS_FIRST 1
-#endif
-
 // Global-address-space views: the nontemporal hint on a flat (generic)
 // pointer is dropped by the backend (plain global_load_dwordx4), so the
-// streamed shards are accessed through address_space(1) pointers to get `nt`.
+// streamed shards -- each byte touched exactly once -- are accessed through
+// address_space(1) pointers to get `nt` (+2-4%, profiles/r01/tune11_*.jsonl;
+// other cache policies through raw buffer instructions measured no better,
+// profiles/r02/ab_cache_policy_buffer_*.txt).
 typedef const __attribute__((address_space(1))) u32x4* gcu32x4p;
 typedef __attribute__((address_space(1))) u32x4* gu32x4p;
 typedef const __attribute__((address_space(1))) uint8_t* gcu8p;
 typedef __attribute__((address_space(1))) uint8_t* gu8p;
 
 __device__ __forceinline__ u32x4 load_full(const uint8_t* p, bool aligned) {
-    if (aligned) {
-#if HEC_NT_LOAD
-        return __builtin_nontemporal_load((gcu32x4p)(p));
-#else
-        return *reinterpret_cast<const u32x4*>(p);
-#endif
-    }
+    if (aligned) return __builtin_nontemporal_load((gcu32x4p)(p));
     u32x4 v;
     __builtin_memcpy(&v, p, 16);
     return v;
 }
 
 __device__ __forceinline__ void store_full(uint8_t* p, u32x4 v, bool aligned) {
-    if (aligned) {
-#if HEC_NT_STORE
+    if (aligned)
         __builtin_nontemporal_store(v, (gu32x4p)(p));
-#else
-        *reinterpret_cast<u32x4*>(p) = v;
-#endif
-    } else {
+    else
         __builtin_memcpy(p, &v, 16);
-    }
 }
 
 // Streamed access at (uniform shard base) + (lane offset): the base is moved
 // to the global address space before the offset is added, so a 32-bit offset
 // becomes the saddr form (SGPR base + VGPR offset) with no 64-bit VALU math.
-// Measurement variants (Makefile VARIANTS): HEC_LOAD_CPOL / HEC_STORE_CPOL >= 0
-// route 32-bit-offset accesses through raw buffer instructions with that
-// cache-policy word (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
-#ifndef HEC_LOAD_CPOL
-#define HEC_LOAD_CPOL -1
-#endif
-#ifndef HEC_STORE_CPOL
-#define HEC_STORE_CPOL -1
-#endif
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t shard_rsrc(const uint8_t* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, int(0xFFFFFFFFu), 0x00020000);
-}
 template <typename OffT>
 __device__ __forceinline__ u32x4 load_at(const uint8_t* base, OffT o) {
-    if constexpr (sizeof(OffT) == 4 && HEC_LOAD_CPOL >= 0)
-        return __builtin_amdgcn_raw_buffer_load_b128(shard_rsrc(base), o, 0, HEC_LOAD_CPOL);
-#if HEC_NT_LOAD
     return __builtin_nontemporal_load((gcu32x4p)((gcu8p)(base) + o));
-#else
-    return *(gcu32x4p)((gcu8p)(base) + o);
-#endif
 }
 template <typename OffT>
 __device__ __forceinline__ void store_at(uint8_t* base, OffT o, u32x4 v) {
-    if constexpr (sizeof(OffT) == 4 && HEC_STORE_CPOL >= 0) {
-        __builtin_amdgcn_raw_buffer_store_b128(v, shard_rsrc(base), o, 0, HEC_STORE_CPOL);
-        return;
-    }
-#if HEC_NT_STORE
     __builtin_nontemporal_store(v, (gu32x4p)((gu8p)(base) + o));
-#else
-    *(gu32x4p)((gu8p)(base) + o) = v;
-#endif
 }
 
 __device__ __noinline__ u32x4 load_tail(const uint8_t* p, uint64_t avail) {
@@ -415,12 +367,11 @@ __device__ __forceinline__ void rs104_chunk(const uint8_t* in_b, uint8_t* out_b,
         u32x4 d[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) d[i] = load_at(in_b + uint64_t(in_id[i]) * in_shard, o);
-#if HEC_LOADS_FIRST
         // all ten loads in flight before any math: without this fence the
         // scheduler interleaves them with the table multiply two at a time
-        // (36 VGPRs, but one wave then waits on HBM five times per chunk)
+        // (36 VGPRs, but one wave then waits on HBM five times per chunk;
+        // -5% decode time with it, profiles/r02/ab_loads_first.txt)
         __builtin_amdgcn_sched_barrier(0);
-#endif
         // opaque here: the table address math (and so the wait for the plan
         // lookup) cannot be hoisted above the data loads
         if constexpr (DEC) {
@@ -515,9 +466,7 @@ __device__ __forceinline__ void rs104_narrow_chunk(const uint8_t* in_b, uint8_t*
         for (int i = 0; i < K; ++i)
             d[i] = __builtin_nontemporal_load(
                 (const __attribute__((address_space(1))) V*)((gcu8p)(in_b + uint64_t(in_id[i]) * in_shard) + o));
-#if HEC_LOADS_FIRST
         __builtin_amdgcn_sched_barrier(0);  // all ten loads in flight before the math
-#endif
         asm volatile("" : "+s"(plan));
         cu32p tab = tabs + plan * (K * R * 5);
         V acc[R];

@@ -40,14 +40,8 @@ namespace hec {
 namespace {
 
 constexpr int K = 10, M = 4, N = 14;
-#ifndef HEC_FILE_SLOTS
-#define HEC_FILE_SLOTS 3
-#endif
-#ifndef HEC_FILE_BATCH_MIB
-#define HEC_FILE_BATCH_MIB 256
-#endif
-constexpr int kSlots = HEC_FILE_SLOTS;                                  // pipeline depth (build-time, measurement)
-constexpr uint64_t kBatchBytes = uint64_t(HEC_FILE_BATCH_MIB) << 20;  // data bytes per GPU job
+constexpr int kSlots = 3;                      // pipeline depth (profiles/r01/ab_file_pipeline_depth.txt)
+constexpr uint64_t kBatchBytes = 256ull << 20;  // data bytes per GPU job
 constexpr uint64_t kLargeSlice = 16ull << 20;   // per-shard slice of a large row
 constexpr int kIoThreads = 16;
 
@@ -93,29 +87,15 @@ void io_error(ErrorSlot& e, const std::string& what) {
 // ---------------------------------------------------------------------------
 // Small fixed thread pool with fork/join task groups.
 // ---------------------------------------------------------------------------
-// Bind the file layer's I/O and writer threads to the device's NUMA node?
-// Off: measured on the GPU box (profiles/r04/file_pool_bind_ab.jsonl,
-// profiles/r04/INDEX.md) a 12 GiB encode ran 25.3-28.6 GiB/s
-// bound against 28.9-30.1 unbound -- the .dat and shard pages in the page
-// cache sit on whichever node, and these threads touch them more than the
-// pinned slots. HEC_FILE_POOL_BIND=1 turns it on (measurement only).
-bool file_threads_bind() {
-    static const bool on = [] {
-        const char* v = std::getenv("HEC_FILE_POOL_BIND");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
-
+// The file layer's I/O and writer threads are left unbound: bound to the
+// GPU's NUMA node a 12 GiB encode ran 25.3-28.6 GiB/s against 28.9-30.1
+// unbound (profiles/r04/file_pool_bind_ab.jsonl) -- the .dat and shard pages
+// in the page cache sit on whichever node, and these threads touch them more
+// than the pinned slots.
 class Pool {
    public:
-    // dev >= 0: workers bind themselves to that device's NUMA node.
-    Pool(int n, int dev) {
-        for (int i = 0; i < n; ++i)
-            th_.emplace_back([this, dev] {
-                if (dev >= 0) (void)hec_bind_thread_to_device(dev, nullptr);  // placement only
-                loop();
-            });
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
     }
     ~Pool() {
         {
@@ -261,7 +241,7 @@ struct StageClock {
 // small volumes do not pay for pinned allocation, streams and threads).
 class FilePipeline {
    public:
-    explicit FilePipeline(int dev) : pool_(kIoThreads, file_threads_bind() ? dev : -1), bind_dev_(dev) {}
+    FilePipeline() : pool_(kIoThreads) {}
     // Grow the slots to at least these sizes; call only while idle.
     int ensure(uint64_t host_bytes, uint64_t dev_bytes) {
         HEC_HIP(hipGetDevice(&dev_id_));
@@ -284,10 +264,7 @@ class FilePipeline {
         host_cap_ = std::max(host_cap_, host_bytes);
         dev_cap_ = std::max(dev_cap_, dev_bytes);
         if (!writer_.joinable())
-            writer_ = std::thread([this] {
-                if (file_threads_bind()) (void)hec_bind_thread_to_device(bind_dev_, nullptr);
-                writer_loop();
-            });
+            writer_ = std::thread([this] { writer_loop(); });
         return HEC_OK;
     }
     // Submit one job (blocks while its slot is still being written).
@@ -410,7 +387,6 @@ class FilePipeline {
     uint64_t host_cap_ = 0, dev_cap_ = 0;
     uint64_t next_ = 0;
     int dev_id_ = 0;
-    int bind_dev_ = 0;
     ErrorSlot err_;
     StageClock clk_;
 };
@@ -433,7 +409,7 @@ int lease_pipeline(uint64_t host_bytes, uint64_t dev_bytes, PipelineLease& out) 
     {
         std::lock_guard<std::mutex> lk(reg_mu);
         auto& slot = (*reg)[dev];
-        if (!slot.first) slot = {new std::mutex(), new FilePipeline(dev)};
+        if (!slot.first) slot = {new std::mutex(), new FilePipeline()};
         e = slot;
     }
     out.lock = std::unique_lock<std::mutex>(*e.first);  // one file operation per device at a time
@@ -456,10 +432,9 @@ struct Rs104 {
 // Skipped on tmpfs, where fallocate zero-fills the page cache up front and
 // the writes then copy over it (12 GiB volume in /dev/shm: 0.37-0.40 s fresh
 // without, 0.47-0.65 s with; profiles/r01/ab_prealloc.txt). Filesystems without
-// fallocate are skipped silently. HEC_NO_PREALLOC=1 turns it off (measurement).
+// fallocate are skipped silently.
 std::shared_future<void> preallocate_async(const int* fds, int n, uint64_t bytes) {
-    static const bool disabled = std::getenv("HEC_NO_PREALLOC") != nullptr;
-    if (disabled || bytes == 0) return {};
+    if (bytes == 0) return {};
     constexpr long kTmpfsMagic = 0x01021994;
     std::vector<int> v;
     for (int i = 0; i < n; ++i) {

@@ -69,14 +69,12 @@ namespace {
 class HostPool {
    public:
     // Workers of device `dev`'s pool run on that GPU's NUMA node (when the
-    // platform says which; they copy into and out of its pinned staging).
-    // HEC_HOST_POOL_BIND=0 leaves them unbound (measurement only).
+    // platform says which; they copy into and out of its pinned staging;
+    // profiles/r04/host_pool_bind_ab.jsonl).
     HostPool(unsigned n, int dev) {
-        const char* v = std::getenv("HEC_HOST_POOL_BIND");
-        const bool bind = !(v && v[0] == '0');
         for (unsigned i = 0; i < n; ++i)
-            th_.emplace_back([this, dev, bind] {
-                if (bind) (void)hec_bind_thread_to_device(dev, nullptr);  // placement only: no-op when unknown
+            th_.emplace_back([this, dev] {
+                (void)hec_bind_thread_to_device(dev, nullptr);  // placement only: no-op when unknown
                 loop();
             });
     }

@@ -44,7 +44,6 @@ def c_abi_call(H, rs, fulls, erased, n_s, reps=1):
 def c_abi_leg(H, rs, fulls, erased, payload, args, out):
     ok, ts = c_abi_call(H, rs, fulls, erased, args.n, args.reps)
     med = float(np.median(ts))
-    out["host_pool_bind"] = os.environ.get("HEC_HOST_POOL_BIND", "1")
     out["gpu_batch_c_abi"] = {"first_s": round(ts[0], 4), "median_s": round(med, 4), "reps": len(ts),
                               "intervals_per_s": round(args.n / med, 1), "payload_GiB_s": round(payload / med / 2**30, 3)}
     out["identical_outputs"] = bool(ok)

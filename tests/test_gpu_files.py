@@ -231,6 +231,53 @@ def test_rebuild_with_every_shard_missing(gpu, tmp_path):
     assert _tree(str(tmp_path / "none_oracle")) == {i: b"" for i in range(14)}
 
 
+def test_randomised_rebuild_size_rules_vs_oracle(gpu, tmp_path):
+    """Seeded sweep of rebuild_ec_files over present shards whose sizes break
+    the equal-rows rule in every way the reference's loop distinguishes
+    (encoder.rs:262-306, reads in shard order per 1 MiB row): a shard a row
+    short, a shard cut mid-row, a shard extended by a few bytes, an empty
+    shard, placed first, in the middle or last among the present ones, 1-4
+    shards lost. The product and the oracle's restatement must agree on the
+    outcome -- the rebuilt ids, or the error and its (expected, actual)
+    payload -- and on every byte of every file afterwards."""
+    import helyim_amd as H
+    rng = np.random.default_rng(2606)
+    rs = O.ReedSolomon(10, 4)
+    M = 1 << 20
+    for case in range(24):
+        L = int(rng.choice([M, 2 * M, 3 * M, 2 * M + 4096, M + 17]))
+        sh = [O.splitmix64_bytes(1000 * case + i, L) for i in range(10)] + [np.zeros(L, np.uint8) for _ in range(4)]
+        rs.encode(sh)
+        lost = sorted(int(i) for i in rng.choice(14, int(rng.integers(1, 5)), replace=False))
+        present = [i for i in range(14) if i not in lost]
+        edits = {}
+        for _ in range(int(rng.integers(0, 3))):
+            i = int(rng.choice([present[0], present[len(present) // 2], present[-1]]))
+            edits[i] = int(rng.choice([max(L - M, 0), L - 5, L + 3, 0, M // 2]))
+        bases = [str(tmp_path / f"{n}{case}") for n in ("a", "b")]
+        for base in bases:
+            for i in present:
+                data = sh[i].tobytes()
+                if i in edits:
+                    n = edits[i]
+                    data = data[:n] if n <= L else data + bytes(n - L)
+                open(base + H.to_ext(i), "wb").write(data)
+        try:
+            got = ("ok", H.rebuild_ec_files(bases[0]))
+        except H.UnexpectedEcShardSize as e:
+            got = ("size", (e.expected, e.actual))
+        except H.ErasureCoding as e:
+            got = ("rs", type(e.inner).__name__)
+        try:
+            want = ("ok", O.rebuild_ec_files(bases[1]))
+        except O.UnexpectedEcShardSize as e:
+            want = ("size", tuple(e.args))
+        except O.TooFewShardsPresent:
+            want = ("rs", "TooFewShardsPresent")
+        assert got == want, (case, L, lost, edits, got, want)
+        assert _tree(bases[0]) == _tree(bases[1]), (case, L, lost, edits)
+
+
 def test_device_selection_and_concurrent_volumes(gpu, golden, tmp_path):
     """hec_set_device per thread (hec.h): volumes encoded and rebuilt
     concurrently from several threads, round-robin over the visible devices

@@ -234,6 +234,42 @@ def test_degraded_read_vs_oracle(gpu, tmp_path, lost):
 
 
 @pytest.mark.gpu
+def test_degraded_read_sweep_vs_oracle(gpu, tmp_path):
+    """Seeded sweep of the degraded read (erasure_coding/mod.rs:303-491 with
+    locate.rs) over volume sizes -- small rows only, large + small rows, and
+    sizes where locate.rs's two large-row counts disagree (:39-40 vs :84) --
+    and 0-5 lost shards, data and parity: every range is read alone and
+    compared with the C oracle's outcome (bytes, Io, TooFewShardsPresent),
+    then all the ranges that succeed are read again as one batch (one GPU
+    round trip for every lost interval)."""
+    import helyim_amd as H
+    rng = np.random.default_rng(403491)
+    for case in range(12):
+        size = int(rng.choice([int(rng.integers(100, 6400)), int(rng.integers(6401, 40000)),
+                               6400 * 2 + int(rng.integers(3000, 6400))]))
+        base, dat = _volume(tmp_path, size, seed=50 + case, name=f"s{case}")
+        lost = sorted(int(i) for i in rng.choice(14, int(rng.integers(0, 6)), replace=False))
+        _drop(base, lost)
+        ranges = _ranges(rng, size, 40, maxlen=2500)
+        ok = []
+        for r in ranges:
+            rc, want = corc.read_ec_data(base, [r], LARGE, SMALL)
+            if rc == 0:
+                assert H.read_ec_data(base, [r], LARGE, SMALL) == want == dat[r[0]:r[0] + r[1]], (case, r)
+                ok.append(r)
+            elif rc == -4:
+                with pytest.raises(H.ErasureCoding) as ei:
+                    H.read_ec_data(base, [r], LARGE, SMALL)
+                assert isinstance(ei.value.inner, H.TooFewShardsPresent), (case, r)
+            else:
+                assert rc == -1, (case, r, rc)
+                with pytest.raises(H.Io):
+                    H.read_ec_data(base, [r], LARGE, SMALL)
+        if ok:
+            assert H.read_ec_data(base, ok, LARGE, SMALL) == b"".join(dat[o:o + n] for o, n in ok), case
+
+
+@pytest.mark.gpu
 def test_degraded_needle_reads(gpu, tmp_path):
     import helyim_amd as H
     base, dat, entries = _needle_volume(tmp_path, n_needles=120)

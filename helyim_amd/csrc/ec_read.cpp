@@ -227,8 +227,16 @@ int read_ranges(const std::string& base, const Shards& sh, uint64_t large, uint6
         uint8_t* dst;
     };
     std::vector<Lost> lost;
+    std::vector<CompactJob> jobs;
     std::vector<hec_interval> ivs;
     uint8_t* dst = out;
+    // Intervals in the reference's order (read_ec_shard_intervals walks them
+    // one by one with `?`, erasure_coding/mod.rs:311-325): the first interval
+    // that fails decides the error. A local interval is read here; a lost one
+    // is checked here -- recover_one_remote_ec_shard_interval counts another
+    // shard as present when its read of the same range returns the full
+    // length, i.e. its file reaches off + size (mod.rs:461), and fails with
+    // TooFewShardsPresent below 10 -- and rebuilt later in one GPU batch.
     for (size_t r = 0; r < n; ++r) {
         ivs.clear();
         if ((rc = locate(large, small, data_size, offsets[r], sizes[r], ivs))) return rc;
@@ -241,29 +249,24 @@ int read_ranges(const std::string& base, const Shards& sh, uint64_t large, uint6
                 if (uint64_t(got) != iv.size)
                     return fail(HEC_ERR_IO, "read " + shard_name(base, id) + ": failed to fill whole buffer");
             } else {
+                uint32_t mask = 0;
+                for (int i = 0; i < kTotalShards; ++i)
+                    if (i != id && sh.fd[i] >= 0 && sh.size[i] >= off + iv.size) mask |= 1u << i;
+                if (__builtin_popcount(mask) < int(kDataShards))
+                    return fail(HEC_ERR_TOO_FEW_SHARDS_PRESENT, "recovering shard " + std::to_string(id) +
+                                                                    " interval at " + std::to_string(off) + ": " +
+                                                                    std::to_string(__builtin_popcount(mask)) +
+                                                                    " shards present");
                 lost.push_back({id, off, iv.size, dst});
+                jobs.push_back(CompactJob{iv.size, mask});
             }
             dst += iv.size;
         }
     }
     if (lost.empty()) return HEC_OK;
-    // recover_one_remote_ec_shard_interval: another shard counts as present when
-    // its read of the same range returns the full length, i.e. its file reaches
-    // off + size. The decode reads the first 10 of them, pread straight into
-    // pinned staging; the rebuilt interval is copied to its place in out.
-    std::vector<CompactJob> jobs(lost.size());
-    for (size_t j = 0; j < lost.size(); ++j) {
-        const Lost& l = lost[j];
-        uint32_t mask = 0;
-        for (int i = 0; i < kTotalShards; ++i)
-            if (i != l.shard && sh.fd[i] >= 0 && sh.size[i] >= l.off + l.size) mask |= 1u << i;
-        if (__builtin_popcount(mask) < int(kDataShards))
-            return fail(HEC_ERR_TOO_FEW_SHARDS_PRESENT, "recovering shard " + std::to_string(l.shard) +
-                                                            " interval at " + std::to_string(l.off) + ": " +
-                                                            std::to_string(__builtin_popcount(mask)) +
-                                                            " shards present");
-        jobs[j] = CompactJob{l.size, mask};
-    }
+    // The decode reads the first 10 present shards of each lost interval,
+    // pread straight into pinned staging; the rebuilt interval is copied to its
+    // place in out.
     return compact_reconstruct_104(
         rs104(), jobs,
         [&](size_t j, int, int shard, uint8_t* dst) {

@@ -148,6 +148,29 @@ def test_read_quirk_volume_matches_oracle(tmp_path):
     assert H.read_ec_data(base, [(100, 1000)], LARGE, SMALL) == dat[100:1100]  # large rows are fine
 
 
+def test_read_error_follows_interval_order_host_only(tmp_path):
+    """read_ec_shard_intervals walks a range's intervals in order with `?`
+    (erasure_coding/mod.rs:311-325), so the FIRST failing interval decides the
+    error. On a volume where locate.rs's two large-row counts disagree, every
+    small-row interval lands past the shard ends: a range whose first interval
+    is on a lost shard fails TooFewShardsPresent (its recovery finds no other
+    shard reaching that far, mod.rs:461) even though its next interval, on a
+    present shard, would fail Io -- decided before any device work, so no GPU
+    is needed. The C oracle agrees."""
+    import helyim_amd as H
+    base, dat = _volume(tmp_path, 5863, seed=53)  # 608-byte shards, data_size 6080: large_block_rows 1 vs 0
+    _drop(base, [8, 11])
+    r = (5078, 495)  # block 158 -> shard 8 (lost) first, then shard 9 (present)
+    assert corc.read_ec_data(base, [r], LARGE, SMALL)[0] == -4
+    with pytest.raises(H.ErasureCoding) as ei:
+        H.read_ec_data(base, [r], LARGE, SMALL)
+    assert isinstance(ei.value.inner, H.TooFewShardsPresent)
+    r2 = (5090, 100)  # block 159 -> shard 9 (present) first: Io, as the oracle
+    assert corc.read_ec_data(base, [r2], LARGE, SMALL)[0] == -1
+    with pytest.raises(H.Io):
+        H.read_ec_data(base, [r2], LARGE, SMALL)
+
+
 def test_read_errors_host_only(tmp_path):
     import helyim_amd as H
     with pytest.raises(H.ShardNotFound):

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT, has_gpu
+from oracle import rs_oracle as O
 
 HEADER = os.path.join(ROOT, "include", "hec.h")
 
@@ -218,6 +219,58 @@ def test_kernel_selection_follows_the_shard_length():
     assert lib.hec_encode_kernel_name(4096).decode().startswith("rs104_kernel<DEC=false>")
     assert lib.hec_encode_kernel_name(17).decode().startswith("rs104_kernel<DEC=false>")
     assert lib.hec_set_host_zero_copy(0) == 0 and lib.hec_set_host_zero_copy(1) == 0
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (3, 2)])
+def test_argument_errors_match_the_oracle_sweep(k, m):
+    """Seeded sweep of the per-call API's argument checks against the
+    oracle's restatement of upstream's (slot count, then each present shard
+    in index order: EmptyShard, IncorrectShardSize; then all present -> no-op,
+    then TooFewShardsPresent): random slot counts, absent slots, empty and
+    off-by-one shards, for reconstruct, reconstruct_data, encode and verify.
+    Every check precedes device work, so the error (or its absence) is
+    compared here without a GPU; where the oracle accepts the input, libhec
+    either needs no device (all present) or reports that it has none."""
+    import helyim_amd as H
+    rng = np.random.default_rng(1000 * k + m)
+    n = k + m
+    hrs, ors = H.ReedSolomon(k, m), O.ReedSolomon(k, m)
+    gpu = has_gpu()
+    for case in range(400):
+        cnt = int(rng.choice([n, n, n, n - 1, n + 1]))
+        L = int(rng.integers(1, 40))
+        slots = []
+        for _ in range(cnt):
+            r = rng.random()
+            if r < 0.25:
+                slots.append(None)
+            elif r < 0.3:
+                slots.append(np.zeros(0, np.uint8))
+            elif r < 0.35:
+                slots.append(np.zeros(L + int(rng.choice([-1, 1])), np.uint8) if L > 1 else np.zeros(L + 1, np.uint8))
+            else:
+                slots.append(rng.integers(0, 256, L, dtype=np.uint8))
+        for op in ("reconstruct", "reconstruct_data", "encode", "verify"):
+            if op in ("encode", "verify"):
+                arg = [s if s is not None else np.zeros(L, np.uint8) for s in slots]
+            else:
+                arg = list(slots)
+            try:
+                getattr(ors, op)([None if s is None else s.copy() for s in arg])
+                want = None
+            except Exception as e:  # the oracle's upstream error classes
+                want = type(e).__name__
+            try:
+                getattr(hrs, op)([None if s is None else s.copy() for s in arg])
+                got = None
+            except H.DeviceError:
+                got = "no device"
+            except H.Error as e:
+                got = type(e).__name__
+            if want is None:
+                assert got is None or (got == "no device" and not gpu), (case, op, got)
+            else:
+                assert got == want, (case, op, cnt, [None if s is None else len(s) for s in slots], got, want)
 
 
 def test_strided_batch_geometry_checked_before_device():

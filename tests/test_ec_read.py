@@ -292,6 +292,72 @@ def test_degraded_read_sweep_vs_oracle(gpu, tmp_path):
             assert H.read_ec_data(base, ok, LARGE, SMALL) == b"".join(dat[o:o + n] for o, n in ok), case
 
 
+def _outcome_h(H, fn):
+    try:
+        return ("ok", fn())
+    except H.NeedleNotFound:
+        return ("deleted", None)
+    except H.ErasureCoding as e:
+        return ("rs", type(e.inner).__name__)
+    except H.Io:
+        return ("io", None)
+
+
+def _outcome_o(fn):
+    try:
+        return ("ok", fn())
+    except O.NeedleNotFound:
+        return ("deleted", None)
+    except O.RSError as e:
+        return ("rs", type(e).__name__)
+    except O.IoError:
+        return ("io", None)
+
+
+@pytest.mark.gpu
+def test_degraded_needle_read_sweep_vs_oracle(gpu, tmp_path):
+    """Seeded sweep of read_ec_shard_needle (erasure_coding/mod.rs:129-171):
+    needle volumes of several sizes, needles deleted after EC (.ecj applied
+    to .ecx), absent ids, 0-5 lost shards. Every needle read alone must give
+    the oracle's outcome -- its bytes, NeedleNotFound (deleted), Io (absent
+    id or a short read), TooFewShardsPresent -- and the batched read of the
+    ids whose reads succeed or are not found must give the same statuses and
+    bytes in one call."""
+    import helyim_amd as H
+    rng = np.random.default_rng(129171)
+    for case in range(8):
+        vdir = tmp_path / f"n{case}"
+        vdir.mkdir()
+        base, dat, entries = _needle_volume(vdir, n_needles=int(rng.integers(6, 80)), seed=300 + case)
+        dels = [entries[int(i)][0] for i in rng.choice(len(entries), int(rng.integers(0, 4)), replace=False)]
+        with open(base + ".ecj", "ab") as f:
+            for k in dels:
+                f.write(struct.pack(">Q", k))
+        O.rebuild_ecx_file(base)
+        lost = sorted(int(i) for i in rng.choice(14, int(rng.integers(0, 6)), replace=False))
+        _drop(base, lost)
+        ids = [k for k, _, _ in entries] + [int(x) for x in rng.integers(1, 10 ** 6, 3)]
+        solo = {}
+        for k in ids:
+            got = _outcome_h(H, lambda: H.read_ec_needle(base, k, LARGE, SMALL))
+            want = _outcome_o(lambda: O.read_ec_needle(base, k, LARGE, SMALL))
+            assert got == want, (case, lost, k, got[0], want[0])
+            solo[k] = got
+        for k, off, size in entries:
+            if solo[k][0] == "ok":
+                assert solo[k][1] == _needle_bytes(dat, off, size), (case, k)
+        batch_ids = [k for k in ids if solo[k][0] in ("ok", "deleted") or k not in {e[0] for e in entries}]
+        res = H.read_ec_needles(base, batch_ids, LARGE, SMALL)
+        for k, r in zip(batch_ids, res):
+            kind = solo[k][0]
+            if kind == "ok":
+                assert r == solo[k][1], (case, k)
+            elif kind == "deleted":
+                assert isinstance(r, H.NeedleNotFound), (case, k)
+            else:
+                assert isinstance(r, H.Io), (case, k)
+
+
 @pytest.mark.gpu
 def test_degraded_needle_reads(gpu, tmp_path):
     import helyim_amd as H

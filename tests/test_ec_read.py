@@ -239,6 +239,49 @@ def test_read_needles_batch_host_only(tmp_path):
     assert H.read_ec_needles(base, [], LARGE, SMALL) == []
 
 
+def test_default_geometry_entry_points_host_only(tmp_path):
+    """hec_read_ec_needle and hec_ec_volume_open take the reference's own
+    1 GiB / 1 MiB blocks (ERASURE_CODING_*_BLOCK_SIZE, lib.rs:44-50): on a
+    volume coded at those blocks they read what the _ex forms read, and what
+    the oracle reads, with every shard present (no GPU)."""
+    import ctypes
+    import helyim_amd as H
+    rng = np.random.default_rng(44)
+    base = str(tmp_path / "d")
+    entries, pos = [], 8
+    for nid in range(1, 30):
+        size = int(rng.integers(0, 200_000))
+        body = 16 + size + 4
+        entries.append((nid * 11, pos // 8, size))
+        pos += body + (8 - body % 8)
+    dat = O.splitmix64_bytes(77, pos + 8).tobytes()
+    open(base + ".dat", "wb").write(dat)
+    assert corc.write_ec_files(base, 256 << 10, H.ERASURE_CODING_LARGE_BLOCK_SIZE,
+                               H.ERASURE_CODING_SMALL_BLOCK_SIZE) == 0
+    open(base + ".idx", "wb").write(b"".join(struct.pack(">QIi", k, o, s) for k, o, s in entries))
+    O.write_sorted_file_from_index(base)
+    lib = H.lib
+    vol = ctypes.c_void_p()
+    assert lib.hec_ec_volume_open(base.encode(), ctypes.byref(vol)) == 0
+    try:
+        for k, off, size in entries:
+            want = _needle_bytes(dat, off, size)
+            assert O.read_ec_needle(base, k) == want
+            buf = ctypes.create_string_buffer(len(want))
+            n = ctypes.c_size_t()
+            assert lib.hec_read_ec_needle(base.encode(), k, buf, len(want), ctypes.byref(n)) == 0
+            assert buf.raw[:n.value] == want
+            buf2 = ctypes.create_string_buffer(len(want))
+            assert lib.hec_ec_volume_read_needle(vol, k, buf2, len(want), ctypes.byref(n)) == 0
+            assert buf2.raw[:n.value] == want
+        n = ctypes.c_size_t()
+        assert lib.hec_read_ec_needle(base.encode(), 5, None, 0, ctypes.byref(n)) == H.Io.code
+        assert lib.hec_ec_volume_read_needle(vol, entries[0][0], None, 0, ctypes.byref(n)) != 0
+        assert n.value == len(_needle_bytes(dat, entries[0][1], entries[0][2]))
+    finally:
+        lib.hec_ec_volume_close(vol)
+
+
 # ---- degraded reads: lost data shards rebuilt on the GPU ---------------------
 
 @pytest.mark.gpu
